@@ -1,0 +1,200 @@
+"""Benchmark: SPGG hot path on MI355X, agent-steps/s (+ roofline, CPU baseline).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3] [--rng philox]
+
+A "step" is one iteration of the reference's run loop (src/model/spgg.py:368-592)
+over every replica of the batch resident in HBM.  Default workload is cfg3 of
+BASELINE.json (L=200, r in {2.0..5.0} x kappa in {0,0.5,1.0} x 5 seeds = 105
+replicas, M=1, reputation state, w_P=1.0) — the L=200 single-GPU configuration
+the metric and its roofline target are quoted on.  Under torchrun each rank runs
+its own batch (seeds offset by rank: weak scaling); the only collective is the
+final cooperation-rate gather (RCCL all_gather).
+
+value = executed agent-steps of all ranks / max-over-ranks wall time of the K
+timed steps (absorbed replicas stop contributing, as in the reference).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-steps/sec (L×L×iters×replicas) + achieved HBM GB/s, L=200"
+ALGO_BYTES_PER_AGENT_STEP = 58.0   # S 1+1, R 8+8, Q 32 read + 8 written
+HBM_PEAK_GBS = 8000.0              # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def runner_params(**kw):
+    from spgg_amd.engine import ReplicaParams
+    base = dict(c=1, cost=1, alpha=0.8, gamma=0.9, epsilon=0.5, epsilon_decay=0.99,
+                epsilon_min=0.01, lambda_epsilon=0.01, delta_R_D=1, R_min=-10, R_max=10,
+                rep_gain_C=1.0, reward_weight_payoff=0.95, influence_factor=1.0, r=3.0)
+    base.update(kw)
+    return ReplicaParams(**base)
+
+
+def workload(name, rank):
+    """(description, L, M2, state, [ReplicaParams]) for a BASELINE.json config."""
+    off = 1000 * rank
+    if name == "cfg2":
+        return ("cfg2: L=200 r=3.0 kappa=1.0 M=1 reputation, 1 replica", 200, False, "reputation",
+                [runner_params(r=3.0, influence_factor=1.0, seed=off)])
+    if name == "cfg3":
+        reps = [runner_params(r=2.0 + 0.5 * i, influence_factor=k, reward_weight_payoff=1.0, seed=off + s)
+                for i in range(7) for k in (0.0, 0.5, 1.0) for s in range(5)]
+        return ("cfg3: L=200 r{2.0..5.0}x kappa{0,0.5,1}x5 seeds = 105 replicas, M=1 reputation, w_P=1.0",
+                200, False, "reputation", reps)
+    if name == "cfg4":
+        return ("cfg4: L=200 r=3.0 kappa=1.0 M=2 action, 8 replicas per GPU", 200, True, "action",
+                [runner_params(r=3.0, influence_factor=1.0, seed=off + s) for s in range(8)])
+    if name == "cfg5":
+        return ("cfg5: L=1000 r=3.6 kappa=1.0 M=1 reputation, 1 replica per GPU", 1000, False, "reputation",
+                [runner_params(r=3.6, influence_factor=1.0, seed=off)])
+    raise SystemExit(f"unknown config {name}")
+
+
+def cpu_baseline(L, M2, state, reps, budget_s=15.0):
+    """Oracle (NumPy restatement of the reference step, same diagnostics) on host cores.
+
+    Bounded sample: up to 16 replicas of the same workload, each run by its own
+    process (the reference's own Pool parallelism, runner.py:142) for as many
+    iterations as fit the budget."""
+    import multiprocessing as mp
+    import numpy as np
+    from oracle import spgg_oracle as O
+    procs = max(1, min(16, os.cpu_count() or 1, len(reps)))
+    # calibrate one step on this host
+    t0 = time.perf_counter()
+    _cpu_job((L, M2, state, reps[0], 3))
+    per_step = (time.perf_counter() - t0) / 3
+    iters = max(5, int(budget_s / max(per_step, 1e-6)))
+    jobs = [(L, M2, state, reps[i % len(reps)], iters) for i in range(procs)]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(procs) as pool:
+        done = pool.map(_cpu_job, jobs)
+    wall = time.perf_counter() - t0
+    agent_steps = sum(done) * L * L
+    return {"value": agent_steps / wall, "unit": "agent-steps/s", "cores": procs, "kind": "port",
+            "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics), {procs} processes x "
+                      f"{iters} iterations of L={L} replicas from the same workload; "
+                      f"{sum(done)} iterations in {wall:.1f}s wall"}
+
+
+def _cpu_job(job):
+    import numpy as np
+    from oracle import spgg_oracle as O
+    L, M2, state, p, iters = job
+    op = O.Params(L=L, iterations=iters, use_second_order=M2, state_representation=state,
+                  **{k: getattr(p, k) for k in ("r", "c", "cost", "alpha", "gamma", "epsilon",
+                                                 "epsilon_decay", "epsilon_min", "influence_factor",
+                                                 "lambda_epsilon", "delta_R_D", "R_min", "R_max",
+                                                 "reward_weight_payoff", "rep_gain_C")})
+    _, fin = O.run(op, np.random.RandomState(p.seed or 0), collect_snapshots=False)
+    return fin["stop_iter"] - 1 if fin["stop_iter"] else iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--rng", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import spgg_amd
+    from spgg_amd.engine import BatchEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    desc, L, M2, state, reps = workload(args.config, rank)
+    K, W = args.steps, args.warmup
+    T = K + W
+    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng)
+    n_agents = len(reps) * L * L
+
+    eng.step(W)
+    torch.cuda.synchronize()
+    stop_w = eng.stop_iter.cpu().numpy().copy()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    eng.step(K)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
+    stop = eng.stop_iter.cpu().numpy()
+    # executed iterations in the timed window [W+1, W+K] per replica
+    last = np.where(stop == 0, W + K, stop - 1)
+    executed = np.clip(last - W, 0, K)
+    agent_steps = float(executed.sum()) * L * L
+
+    # final cooperation-rate gather over RCCL (the path's only collective)
+    ncoop = eng.stats[:, :, 0].cpu().numpy()          # SPGG_ST_NCOOP per iteration slot
+    coop = torch.from_numpy(np.array([ncoop[k, int(last[k]) + 1] / (L * L) for k in range(len(reps))]))
+    coop = coop.to(torch.device("cuda", local))
+    tot = torch.tensor([agent_steps, wall], dtype=torch.float64, device=coop.device)
+    if dist:
+        gathered = [torch.empty_like(coop) for _ in range(world)]
+        dist.all_gather(gathered, coop)
+        s = tot[:1].clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        w = tot[1:].clone()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        agent_steps_all, wall_max = float(s.item()), float(w.item())
+    else:
+        agent_steps_all, wall_max = agent_steps, wall
+    value = agent_steps_all / wall_max
+    per_step_dev_s = dev_ms / 1e3 / K
+    step_agents = agent_steps / K
+    achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": wall_max * 1e3 / K,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (reference init: S~Bernoulli(1/2), R=0, Q~U(-0.01,0.01))",
+            "config": {"workload": desc, "L": L, "replicas_per_gpu": len(reps),
+                       "agents_per_gpu": n_agents, "second_order": M2, "state": state,
+                       "rng": args.rng, "parallelism": f"replicas sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "act+learn (one iteration)",
+                         "device_ms_per_step": per_step_dev_s * 1e3},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(L, M2, state, reps, args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

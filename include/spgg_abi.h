@@ -1,0 +1,173 @@
+/*
+ * spgg_abi.h — C ABI of libspgg_hip.so, the MI355X (gfx950) implementation of
+ * the SPGG per-iteration hot path.
+ *
+ * Replaces, per executed iteration of the reference's run loop:
+ *   - payoff of the 5 overlapping groups      src/model/spgg.py:23-36, 230-279, 373-378
+ *   - state representation (reputation/action) src/model/spgg.py:281-317, 409, 423
+ *   - eps-greedy action select                 src/model/algorithms.py:102-110
+ *   - reputation update                        src/model/spgg.py:319-323, 413-416
+ *   - reward                                   src/model/spgg.py:424-427
+ *   - Q-learning TD update                     src/model/algorithms.py:112-133
+ *   - diagnostic TD + neighbor-influence term  src/model/spgg.py:445-509
+ *   - per-step history reductions              src/model/spgg.py:380-394, 418-420, 511-545, 561-592
+ * The reference has no native layer; this ABI is what its Python would bind
+ * (see INTEGRATION.md for the ctypes binding used by the drop-in SPGG class).
+ *
+ * Conventions: every function returns 0 on success, a negative SPGG_E* code on
+ * failure (detail in spgg_last_error).  No C++ exception crosses the ABI.
+ * Buffers are DEVICE pointers owned by the caller (e.g. torch tensors); the
+ * library only allocates its per-replica parameter table and frees it in
+ * spgg_destroy.  A context is bound to one device and is not thread-safe.
+ * spgg_step / spgg_flush only ENQUEUE work on the given HIP stream.
+ */
+#ifndef SPGG_ABI_H
+#define SPGG_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPGG_ABI_VERSION 1
+
+#define SPGG_OK 0
+#define SPGG_E_ARG (-1)     /* bad argument / shape */
+#define SPGG_E_STATE (-2)   /* call order (e.g. step before bind) */
+#define SPGG_E_HIP (-3)     /* HIP runtime error */
+
+/* state representation (spgg.py:289-310) */
+#define SPGG_STATE_REPUTATION 0
+#define SPGG_STATE_ACTION 1
+
+/* random stream used by the eps-greedy select */
+#define SPGG_RNG_INJECT 0   /* caller fills explore/bit bytes per step (host MT19937 etc.) */
+#define SPGG_RNG_MT19937 1  /* device MT19937, bit-identical to numpy.random.RandomState */
+#define SPGG_RNG_PHILOX 2   /* counter-based Philox4x32-10 keyed by (seed, replica, step, agent) */
+
+/* Per-step history record: stats[rep][t][SPGG_NSTAT] (float64), t = 0 .. iterations+1.
+ * Integer counts are stored exactly as float64. */
+enum {
+  SPGG_ST_NCOOP = 0,      /* #S_t==0 at iteration start (spgg.py:383)            */
+  SPGG_ST_SUMP = 1,       /* sum P                       (spgg.py:388)            */
+  SPGG_ST_SUMP_C = 2,     /* sum P over S_t==0           (spgg.py:389)            */
+  SPGG_ST_SUMP_D = 3,     /* sum P over S_t==1           (spgg.py:390)            */
+  SPGG_ST_SUMR = 4,       /* sum R_t                     (spgg.py:394)            */
+  SPGG_ST_SW_CD = 5,      /* switches C->D               (spgg.py:419)            */
+  SPGG_ST_SW_DC = 6,      /* switches D->C               (spgg.py:420)            */
+  SPGG_ST_SUM_WPP = 7,    /* sum w_P*P                   (spgg.py:425)            */
+  SPGG_ST_SUM_WRR = 8,    /* sum w_rep*rep_reward        (spgg.py:426)            */
+  SPGG_ST_SUM_REW_C = 9,  /* sum reward over a==0        (spgg.py:542)            */
+  SPGG_ST_SUM_REW_D = 10, /* sum reward over a==1        (spgg.py:543)            */
+  SPGG_ST_SUM_RATIO_C = 11, /* sum rep-reward ratio over a==0 (spgg.py:533-535)   */
+  SPGG_ST_GC0 = 12,       /* 12..17: #agents with d defectors in 5-pt group (spgg.py:586-592) */
+  SPGG_ST_NMD_POS = 18,   /* #agents with max_diff > 0   (spgg.py:521)            */
+  SPGG_ST_NMD_POS2 = 19,  /* ... whose best neighbor is second order (spgg.py:520-523) */
+  SPGG_ST_SUM_PCT = 20,   /* sum NI percent              (spgg.py:512-513)        */
+  SPGG_ST_SUMQ = 21,      /* 21..24: sum Q[:,:,s,a] after NI, index 2s+a (spgg.py:562-565) */
+  SPGG_ST_SUMQ_C = 25,    /* 25..28: ... over prev_S==0  (spgg.py:568-577)        */
+  SPGG_ST_SUMQ_D = 29,    /* 29..32: ... over prev_S==1  (spgg.py:579-583)        */
+  SPGG_ST_GMAX = 33,      /* global max |diff| (float64 bits, atomic max) (spgg.py:488) */
+  SPGG_NSTAT = 34
+};
+
+typedef struct spgg_ctx spgg_ctx;
+
+typedef struct {
+  int32_t device;        /* HIP device ordinal */
+  int32_t n_rep;         /* replicas in the batch (independent lattices) */
+  int32_t L;             /* lattice side */
+  int32_t second_order;  /* use_second_order (M=2) */
+  int32_t state_mode;    /* SPGG_STATE_* */
+  int32_t rng_mode;      /* SPGG_RNG_* */
+  int32_t iterations;    /* capacity: stats/eps tables hold iterations+2 slots */
+  int32_t reserved;
+} spgg_config;
+
+/* Per-replica constants, precomputed by the host in the reference's own
+ * (Python float) arithmetic so the device reproduces it bit for bit. */
+typedef struct {
+  double rc;          /* r*c                       (spgg.py:256)  */
+  double cost;        /*                           (spgg.py:256)  */
+  double norm_min;    /* r-5                       (spgg.py:149)  */
+  double norm_den;    /* 4r-(r-5)                  (spgg.py:377)  */
+  double w_p;         /* reward_weight_payoff      (spgg.py:427)  */
+  double w_rep;       /* 1-w_P                     (spgg.py:108)  */
+  double alpha;       /* TD learning rate (algorithm's)  (algorithms.py:131) */
+  double gamma;       /* TD discount (algorithm's)       (algorithms.py:128) */
+  double diag_alpha;  /* SPGG.alpha for the NI percent   (spgg.py:475,512)  */
+  double diag_gamma;  /* SPGG.gamma for the diag TD      (spgg.py:473)      */
+  double kappa;       /* influence_factor          (spgg.py:489)  */
+  double lambda_eps;  /* lambda_epsilon            (spgg.py:489)  */
+  double rep_gain_c;  /* reputation gain on C      (spgg.py:321)  */
+  double neg_delta_r_d; /* -delta_R_D              (spgg.py:321)  */
+  double r_min;
+  double r_max;
+  uint64_t seed;      /* Philox key (SPGG_RNG_PHILOX only) */
+  uint64_t reserved;
+} spgg_rep_params;
+
+/* Device buffers, all replica-major.  n = L*L.
+ *   S[2]      uint8  [n_rep][n]      strategy ping-pong, S_t lives in S[(t-1)&1]
+ *   R[2]      f64    [n_rep][n]      reputation ping-pong, R_t in R[(t-1)&1]
+ *   Q         f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2)
+ *   reward    f64    [n_rep][n]      scratch: reward of the current step
+ *   aux       uint8  [n_rep][n]      scratch: s_old | prevS<<1 | (a*==a)<<2
+ *   ni_md     f64    [n_rep][n]      pending NI: max(0, max_diff)
+ *   ni_atd    f64    [n_rep][n]      pending NI: |alpha*td'| (diagnostic)
+ *   explore   uint8  [n_rep][n]      eps-greedy explore flag of the step (INJECT/MT19937)
+ *   rbit      uint8  [n_rep][n]      random action of the step          (INJECT/MT19937)
+ *   mt_state  uint32 [n_rep][625]    MT19937 key[624] + pos (MT19937 only)
+ *   eps       f64    [n_rep][iterations+2]  eps used by iteration t
+ *   stats     f64    [n_rep][iterations+2][SPGG_NSTAT]  zero-initialised; slot
+ *                                    t0 must hold NCOOP of S_t0 before stepping
+ *   stop_iter int32  [n_rep]         0 while running, else the absorbing iteration
+ */
+typedef struct {
+  uint8_t* S[2];
+  double* R[2];
+  double* Q;
+  double* reward;
+  uint8_t* aux;
+  double* ni_md;
+  double* ni_atd;
+  uint8_t* explore;
+  uint8_t* rbit;
+  uint32_t* mt_state;
+  double* eps;
+  double* stats;
+  int32_t* stop_iter;
+} spgg_buffers;
+
+int spgg_abi_version(void);
+const char* spgg_last_error(const spgg_ctx* ctx);
+
+int spgg_create(spgg_ctx** out, const spgg_config* cfg);
+/* Copies n_rep host records to the device (stream-ordered on the null stream). */
+int spgg_set_params(spgg_ctx* ctx, const spgg_rep_params* params);
+int spgg_bind(spgg_ctx* ctx, const spgg_buffers* bufs);
+
+/* Enqueue iterations t0 .. t0+n_steps-1 (1-based, as the reference's loop
+ * variable i, spgg.py:368).  Replicas that reach an absorbing state stop by
+ * themselves (spgg.py:405-406).  In SPGG_RNG_INJECT mode n_steps must be 1
+ * and the explore/rbit bytes of iteration t0 must already be in place. */
+int spgg_step(spgg_ctx* ctx, int32_t t0, int32_t n_steps, void* hip_stream);
+
+/* Apply the deferred neighbor-influence term of iteration t_last (the last
+ * executed one) and its Q statistics.  Call once after the final spgg_step. */
+int spgg_flush(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
+
+/* Draw the RNG bytes of one iteration only (MT19937 mode; for tests). */
+int spgg_draw(spgg_ctx* ctx, int32_t t, void* hip_stream);
+
+/* P (normalised payoff, spgg.py:373-378) of every agent from S_t into
+ * out[n_rep][n] (device).  Used for SPGG.P and run()'s return value. */
+int spgg_payoff(spgg_ctx* ctx, int32_t t, double* out, void* hip_stream);
+
+int spgg_destroy(spgg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPGG_ABI_H */

@@ -1,0 +1,106 @@
+"""ctypes binding of libspgg_hip.so (C ABI declared in include/spgg_abi.h).
+
+The library is built in-tree by `build.py` (hipcc --offload-arch=gfx950).  There
+is no fallback: if the shared object is missing or cannot be loaded, every entry
+point raises, so a GPU run can never silently take another path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
+
+ABI_VERSION = 1
+OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
+STATE_REPUTATION, STATE_ACTION = 0, 1
+RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
+RNG_MODES = {"inject": RNG_INJECT, "mt19937": RNG_MT19937, "philox": RNG_PHILOX}
+
+# stats record layout (enum in spgg_abi.h)
+ST_NCOOP, ST_SUMP, ST_SUMP_C, ST_SUMP_D, ST_SUMR = 0, 1, 2, 3, 4
+ST_SW_CD, ST_SW_DC, ST_SUM_WPP, ST_SUM_WRR = 5, 6, 7, 8
+ST_SUM_REW_C, ST_SUM_REW_D, ST_SUM_RATIO_C = 9, 10, 11
+ST_GC0, ST_NMD_POS, ST_NMD_POS2, ST_SUM_PCT = 12, 18, 19, 20
+ST_SUMQ, ST_SUMQ_C, ST_SUMQ_D, ST_GMAX = 21, 25, 29, 33
+NSTAT = 34
+
+EXPORTED = ("spgg_abi_version", "spgg_last_error", "spgg_create", "spgg_set_params",
+            "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_destroy")
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("n_rep", ctypes.c_int32), ("L", ctypes.c_int32),
+                ("second_order", ctypes.c_int32), ("state_mode", ctypes.c_int32),
+                ("rng_mode", ctypes.c_int32), ("iterations", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class RepParams(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_double) for name in (
+        "rc", "cost", "norm_min", "norm_den", "w_p", "w_rep", "alpha", "gamma",
+        "diag_alpha", "diag_gamma", "kappa", "lambda_eps", "rep_gain_c", "neg_delta_r_d",
+        "r_min", "r_max")] + [("seed", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+
+
+class Buffers(ctypes.Structure):
+    _fields_ = [("S", ctypes.c_void_p * 2), ("R", ctypes.c_void_p * 2), ("Q", ctypes.c_void_p),
+                ("reward", ctypes.c_void_p), ("aux", ctypes.c_void_p), ("ni_md", ctypes.c_void_p),
+                ("ni_atd", ctypes.c_void_p), ("explore", ctypes.c_void_p), ("rbit", ctypes.c_void_p),
+                ("mt_state", ctypes.c_void_p), ("eps", ctypes.c_void_p), ("stats", ctypes.c_void_p),
+                ("stop_iter", ctypes.c_void_p)]
+
+
+class SpggError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None):
+    """Load (once) and type the shared library; raises if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise SpggError(f"{p} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(p)
+        vp, i32 = ctypes.c_void_p, ctypes.c_int32
+        lib.spgg_abi_version.restype = ctypes.c_int
+        lib.spgg_abi_version.argtypes = []
+        lib.spgg_last_error.restype = ctypes.c_char_p
+        lib.spgg_last_error.argtypes = [vp]
+        lib.spgg_create.restype = ctypes.c_int
+        lib.spgg_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Config)]
+        lib.spgg_set_params.restype = ctypes.c_int
+        lib.spgg_set_params.argtypes = [vp, ctypes.POINTER(RepParams)]
+        lib.spgg_bind.restype = ctypes.c_int
+        lib.spgg_bind.argtypes = [vp, ctypes.POINTER(Buffers)]
+        lib.spgg_step.restype = ctypes.c_int
+        lib.spgg_step.argtypes = [vp, i32, i32, vp]
+        lib.spgg_flush.restype = ctypes.c_int
+        lib.spgg_flush.argtypes = [vp, i32, vp]
+        lib.spgg_draw.restype = ctypes.c_int
+        lib.spgg_draw.argtypes = [vp, i32, vp]
+        lib.spgg_payoff.restype = ctypes.c_int
+        lib.spgg_payoff.argtypes = [vp, i32, vp, vp]
+        lib.spgg_destroy.restype = ctypes.c_int
+        lib.spgg_destroy.argtypes = [vp]
+        v = lib.spgg_abi_version()
+        if v != ABI_VERSION:
+            raise SpggError(f"libspgg_hip ABI {v} != expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, ctx=None, what: str = ""):
+    if rc != OK:
+        lib = load()
+        detail = lib.spgg_last_error(ctx).decode() if ctx else ""
+        raise SpggError(f"{what} failed (rc={rc}): {detail}")

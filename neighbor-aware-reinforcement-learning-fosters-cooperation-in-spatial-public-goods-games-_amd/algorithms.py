@@ -1,0 +1,100 @@
+"""RL operator interface of the reference (src/model/algorithms.py:10-383).
+
+The classes keep the reference's constructor signature, attributes, eps
+schedule (`decay_epsilon`, algorithms.py:40-42) and the `create_algorithm`
+factory with its ValueError.  Their per-lattice `select_action` /
+`update_q_table` arithmetic is fused into the HIP step (libspgg_hip.so) and
+driven by `SPGG.run` / `BatchEngine`; calling those two methods on their own
+raises, because this package has no NumPy execution path by design.
+
+GPU coverage: QLearning (algorithms.py:96-133).  SARSA, ExpectedSARSA and
+DoubleQLearning are accepted by the factory (same names, same errors) but
+`SPGG.run` raises NotImplementedError for them until their kernels land.
+"""
+from __future__ import annotations
+
+from abc import ABC
+from typing import Tuple
+
+import numpy as np
+
+
+class RLAlgorithm(ABC):
+    """Base class (algorithms.py:10-93)."""
+
+    kind = "abstract"
+
+    def __init__(self, alpha: float, gamma: float, epsilon: float,
+                 epsilon_decay: float, epsilon_min: float, **kwargs):
+        self.alpha = alpha
+        self.gamma = gamma
+        self.epsilon = epsilon
+        self.epsilon_decay = epsilon_decay
+        self.epsilon_min = epsilon_min
+
+    def decay_epsilon(self):
+        """algorithms.py:40-42 (host scalar; the device reads the same schedule)."""
+        self.epsilon = max(self.epsilon * self.epsilon_decay, self.epsilon_min)
+
+    def select_action(self, q_table, states, L, **kwargs):
+        raise NotImplementedError(
+            f"{type(self).__name__}.select_action is fused into the HIP step; drive it "
+            "through SPGG.run() or BatchEngine")
+
+    def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
+        raise NotImplementedError(
+            f"{type(self).__name__}.update_q_table is fused into the HIP step; drive it "
+            "through SPGG.run() or BatchEngine")
+
+
+class QLearning(RLAlgorithm):
+    """Off-policy TD with max over next-state actions (algorithms.py:96-133)."""
+    kind = "qlearning"
+
+
+class SARSA(RLAlgorithm):
+    """On-policy TD (algorithms.py:136-178)."""
+    kind = "sarsa"
+
+
+class ExpectedSARSA(RLAlgorithm):
+    """Expected-value TD under the eps-greedy policy (algorithms.py:181-234)."""
+    kind = "expected_sarsa"
+
+
+class DoubleQLearning(RLAlgorithm):
+    """Two Q tables (algorithms.py:237-341)."""
+    kind = "double_qlearning"
+
+    def __init__(self, alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs):
+        super().__init__(alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs)
+        self.q_table_1 = None
+        self.q_table_2 = None
+
+    def initialize_q_tables(self, shape: Tuple[int, ...]):
+        """Two more U(-0.01, 0.01) tables from the global stream (algorithms.py:250-260)."""
+        self.q_table_1 = np.random.uniform(low=-0.01, high=0.01, size=shape)
+        self.q_table_2 = np.random.uniform(low=-0.01, high=0.01, size=shape)
+
+    def get_combined_q_table(self):
+        """Average of both tables (algorithms.py:262-266)."""
+        if self.q_table_1 is None or self.q_table_2 is None:
+            raise ValueError("Q-tables not initialized. Call initialize_q_tables first.")
+        return (self.q_table_1 + self.q_table_2) / 2
+
+
+def create_algorithm(algorithm_name: str, alpha: float, gamma: float,
+                     epsilon: float, epsilon_decay: float, epsilon_min: float,
+                     **kwargs) -> RLAlgorithm:
+    """Factory with the reference's accepted names and error (algorithms.py:344-383)."""
+    algorithm_name = algorithm_name.lower()
+    if algorithm_name in ("qlearning", "q-learning"):
+        return QLearning(alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs)
+    if algorithm_name == "sarsa":
+        return SARSA(alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs)
+    if algorithm_name in ("expected_sarsa", "expected-sarsa"):
+        return ExpectedSARSA(alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs)
+    if algorithm_name in ("double_qlearning", "double-q-learning"):
+        return DoubleQLearning(alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs)
+    raise ValueError(f"Unknown algorithm: {algorithm_name}. "
+                     f"Supported: 'qlearning', 'sarsa', 'expected_sarsa', 'double_qlearning'")

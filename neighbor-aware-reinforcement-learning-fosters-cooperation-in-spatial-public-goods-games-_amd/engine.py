@@ -1,0 +1,408 @@
+"""Batched replica engine: many independent SPGG lattices stepped on one MI355X.
+
+Host side of the hot path.  It owns the device buffers (torch tensors used only
+as HBM allocations), fills the per-replica parameter table with constants
+computed in the reference's own Python-float arithmetic, and drives
+`libspgg_hip.so` through its C ABI (`include/spgg_abi.h`).  The per-step
+history record each replica accumulates on the device is turned back into the
+reference's HDF5 datasets (`src/model/spgg.py:594-633`) by `histories()`.
+
+Random streams:
+  * "mt19937": init draws on the host exactly as SPGG.__init__ does
+    (spgg.py:121,162) from `numpy.random.RandomState`; the continuing MT19937
+    key is moved to the device, which draws every step's rand(L,L) and
+    randint(0,2,(L,L)) (algorithms.py:105,108) bit-identically.
+  * "inject": the host draws each step (tests / debugging).
+  * "philox": counter-based per-agent stream; statistical parity only.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as C
+
+SNAPSHOT_ITERS = (1, 10, 100, 1000, 5000, 10000, 20000, 30000, 40000)  # spgg.py:153
+PNG_ITERS = set(SNAPSHOT_ITERS) | {5000}                                 # spgg.py:553
+
+
+@dataclasses.dataclass
+class ReplicaParams:
+    """Constructor arguments of one replica (spgg.py:50-56 + the RL operator's own)."""
+    r: float = 2
+    c: float = 1
+    cost: float = 0.5
+    alpha: float = 0.1            # SPGG.alpha (diagnostic TD / NI percent, spgg.py:475)
+    gamma: float = 0.9            # SPGG.gamma (diagnostic TD, spgg.py:473)
+    epsilon: float = 0.5          # operator's eps schedule (algorithms.py:40-42)
+    epsilon_decay: float = 0.995
+    epsilon_min: float = 0.01
+    influence_factor: float = 1.0
+    lambda_epsilon: float = 0.01
+    delta_R_D: float = 1
+    R_min: float = -10
+    R_max: float = 10
+    reward_weight_payoff: float = 1.0
+    rep_gain_C: float = 0.5
+    alg_alpha: Optional[float] = None  # operator's alpha if it differs (algorithm instance)
+    alg_gamma: Optional[float] = None
+    seed: Optional[int] = None         # RandomState seed (mt19937/inject) or Philox key
+
+    def to_c(self) -> C.RepParams:
+        p = C.RepParams()
+        r, c = self.r, self.c
+        p.rc = float(r * c)                              # spgg.py:256 (r*c first)
+        p.cost = float(self.cost)
+        norm_max, norm_min = 4 * r, r - 5                # spgg.py:148-149
+        p.norm_min = float(norm_min)
+        p.norm_den = float(norm_max - norm_min)          # spgg.py:377
+        p.w_p = float(self.reward_weight_payoff)
+        p.w_rep = float(1 - self.reward_weight_payoff)   # spgg.py:108
+        p.alpha = float(self.alpha if self.alg_alpha is None else self.alg_alpha)
+        p.gamma = float(self.gamma if self.alg_gamma is None else self.alg_gamma)
+        p.diag_alpha = float(self.alpha)
+        p.diag_gamma = float(self.gamma)
+        p.kappa = float(self.influence_factor)
+        p.lambda_eps = float(self.lambda_epsilon)
+        p.rep_gain_c = float(self.rep_gain_C)
+        p.neg_delta_r_d = float(-self.delta_R_D)
+        p.r_min = float(self.R_min)
+        p.r_max = float(self.R_max)
+        p.seed = int(self.seed or 0) & 0xFFFFFFFFFFFFFFFF
+        return p
+
+
+def epsilon_table(eps0, decay, emin, n):
+    """eps in effect at iterations 1..n (index t), decayed after every step (algorithms.py:42)."""
+    out = np.empty(n + 1)
+    out[0] = eps0
+    e = eps0
+    for t in range(1, n + 1):
+        out[t] = e
+        e = max(e * decay, emin)
+    return out
+
+
+@dataclasses.dataclass
+class InitState:
+    Q: np.ndarray                 # (L, L, 2, 2) float64
+    S: np.ndarray                 # (L, L) int
+    mt_key: Optional[np.ndarray] = None  # (624,) uint32 continuing MT19937 key
+    mt_pos: int = 0
+    rs: Optional[np.random.RandomState] = None  # host stream (inject mode)
+
+
+def reference_init(L: int, rs: np.random.RandomState, S_in_one=None) -> InitState:
+    """SPGG.__init__'s draws: Q ~ U(-0.01, 0.01) then S ~ randint(0,2) (spgg.py:121,162)."""
+    Q = rs.uniform(low=-0.01, high=0.01, size=(L, L, 2, 2))
+    S = rs.randint(0, 2, size=(L, L)) if S_in_one is None else np.asarray(S_in_one)
+    st = rs.get_state()
+    return InitState(Q=Q, S=S, mt_key=np.asarray(st[1], dtype=np.uint32), mt_pos=int(st[2]), rs=rs)
+
+
+class BatchEngine:
+    """n_rep independent replicas of one (L, M, state) configuration on one device."""
+
+    def __init__(self, L: int, iterations: int, replicas: Sequence[ReplicaParams],
+                 use_second_order: bool = True, state_representation: str = "reputation",
+                 rng: str = "mt19937", device=None, init: Optional[Sequence[InitState]] = None):
+        if state_representation not in ("reputation", "action"):
+            raise ValueError(f"Unknown state_representation: {state_representation}. "
+                             f"Must be 'reputation' or 'action'")
+        if rng not in C.RNG_MODES:
+            raise ValueError(f"rng must be one of {sorted(C.RNG_MODES)}")
+        if not torch.cuda.is_available():
+            raise C.SpggError("BatchEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = C.load()
+        self.L, self.n = int(L), int(L) * int(L)
+        self.T = int(iterations)
+        self.reps = list(replicas)
+        self.R = len(self.reps)
+        self.M2 = bool(use_second_order)
+        self.state_rep = state_representation
+        self.rng = rng
+        self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        if init is None:
+            init = [reference_init(self.L, np.random.RandomState(p.seed)) for p in self.reps]
+        self.init = list(init)
+        if len(self.init) != self.R:
+            raise ValueError("one InitState per replica")
+        self._alloc()
+        self._create()
+        self.t = 1                 # next iteration to execute
+        self.stopped = np.zeros(self.R, dtype=np.int64)
+        self.snapshots = [dict() for _ in range(self.R)]
+        self.png_frames = [dict() for _ in range(self.R)]
+        self._flushed = False
+
+    # -- setup ---------------------------------------------------------------
+    def _alloc(self):
+        R, n, T, d = self.R, self.n, self.T, self.dev
+        f64, u8 = torch.float64, torch.uint8
+        S0 = np.stack([np.asarray(s.S).reshape(n) for s in self.init]).astype(np.uint8)
+        Q0 = np.stack([np.asarray(s.Q, dtype=np.float64).reshape(n, 4) for s in self.init])
+        self.S = torch.zeros((2, R, n), dtype=u8, device=d)
+        self.S[0].copy_(torch.from_numpy(S0))
+        self.Rep = torch.zeros((2, R, n), dtype=f64, device=d)
+        self.Q = torch.from_numpy(Q0).to(d).contiguous()
+        self.reward = torch.zeros((R, n), dtype=f64, device=d)
+        self.aux = torch.zeros((R, n), dtype=u8, device=d)
+        self.ni_md = torch.zeros((R, n), dtype=f64, device=d)
+        self.ni_atd = torch.zeros((R, n), dtype=f64, device=d)
+        self.explore = torch.zeros((R, n), dtype=u8, device=d)
+        self.rbit = torch.zeros((R, n), dtype=u8, device=d)
+        mt = np.zeros((R, 625), dtype=np.uint32)
+        if self.rng == "mt19937":
+            for k, s in enumerate(self.init):
+                if s.mt_key is None:
+                    raise ValueError("mt19937 mode needs the continuing MT19937 key of each replica")
+                mt[k, :624] = s.mt_key
+                mt[k, 624] = s.mt_pos
+        self.mt_state = torch.from_numpy(mt.view(np.int32)).to(d)
+        eps = np.zeros((R, T + 2))
+        cache = {}
+        for k, p in enumerate(self.reps):
+            key = (p.epsilon, p.epsilon_decay, p.epsilon_min)
+            if key not in cache:
+                cache[key] = epsilon_table(*key, T + 1)
+            eps[k] = cache[key]
+        self.eps_host = eps
+        self.eps = torch.from_numpy(eps).to(d)
+        self.stats = torch.zeros((R, T + 2, C.NSTAT), dtype=f64, device=d)
+        ncoop = (S0 == 0).sum(axis=1).astype(np.float64)
+        self.stats[:, 1, C.ST_NCOOP] = torch.from_numpy(ncoop).to(d)
+        self.stop_iter = torch.zeros(R, dtype=torch.int32, device=d)
+        self.P_buf = torch.zeros((R, n), dtype=f64, device=d)
+
+    def _create(self):
+        cfg = C.Config(device=self.dev.index, n_rep=self.R, L=self.L, second_order=int(self.M2),
+                       state_mode=C.STATE_ACTION if self.state_rep == "action" else C.STATE_REPUTATION,
+                       rng_mode=C.RNG_MODES[self.rng], iterations=self.T, reserved=0)
+        ctx = __import__("ctypes").c_void_p()
+        C.check(self.lib.spgg_create(__import__("ctypes").byref(ctx), cfg), None, "spgg_create")
+        self.ctx = ctx
+        arr = (C.RepParams * self.R)(*[p.to_c() for p in self.reps])
+        C.check(self.lib.spgg_set_params(self.ctx, arr), self.ctx, "spgg_set_params")
+        b = C.Buffers()
+        b.S[0], b.S[1] = self.S[0].data_ptr(), self.S[1].data_ptr()
+        b.R[0], b.R[1] = self.Rep[0].data_ptr(), self.Rep[1].data_ptr()
+        b.Q = self.Q.data_ptr()
+        b.reward, b.aux = self.reward.data_ptr(), self.aux.data_ptr()
+        b.ni_md, b.ni_atd = self.ni_md.data_ptr(), self.ni_atd.data_ptr()
+        b.explore, b.rbit = self.explore.data_ptr(), self.rbit.data_ptr()
+        b.mt_state = self.mt_state.data_ptr()
+        b.eps, b.stats, b.stop_iter = self.eps.data_ptr(), self.stats.data_ptr(), self.stop_iter.data_ptr()
+        self._bufs = b
+        C.check(self.lib.spgg_bind(self.ctx, b), self.ctx, "spgg_bind")
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.spgg_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    # -- stepping ------------------------------------------------------------
+    def _inject(self, t):
+        """Host draws of iteration t (algorithms.py:105,108) for replicas that execute it."""
+        ncoop = self.stats[:, t, C.ST_NCOOP].cpu().numpy()
+        stop = self.stop_iter.cpu().numpy()
+        ex = np.zeros((self.R, self.n), dtype=np.uint8)
+        rb = np.zeros((self.R, self.n), dtype=np.uint8)
+        for k, s in enumerate(self.init):
+            if stop[k] != 0 or ncoop[k] == 0 or ncoop[k] == self.n:
+                continue
+            u = s.rs.rand(self.L, self.L).reshape(-1)
+            b = s.rs.randint(0, 2, size=(self.L, self.L)).reshape(-1)
+            ex[k] = u < self.eps_host[k, t]
+            rb[k] = b
+        self.explore.copy_(torch.from_numpy(ex))
+        self.rbit.copy_(torch.from_numpy(rb))
+
+    def step(self, n_steps: int):
+        """Enqueue the next n_steps iterations (no host sync except in inject mode)."""
+        n_steps = min(n_steps, self.T - self.t + 1)
+        if n_steps <= 0:
+            return 0
+        if self.rng == "inject":
+            for _ in range(n_steps):
+                self._inject(self.t)
+                C.check(self.lib.spgg_step(self.ctx, self.t, 1, self.stream), self.ctx, "spgg_step")
+                self.t += 1
+        else:
+            C.check(self.lib.spgg_step(self.ctx, self.t, n_steps, self.stream), self.ctx, "spgg_step")
+            self.t += n_steps
+        return n_steps
+
+    def all_stopped(self) -> bool:
+        self.stopped = self.stop_iter.cpu().numpy().astype(np.int64)
+        return bool(np.all(self.stopped != 0))
+
+    def flush(self):
+        """Apply the deferred NI term of the last executed iteration (once, at the end)."""
+        if self._flushed or self.t <= 1:
+            return
+        C.check(self.lib.spgg_flush(self.ctx, self.t - 1, self.stream), self.ctx, "spgg_flush")
+        self._flushed = True
+
+    def run(self, chunk: int = 256, snapshots: bool = True, png: bool = False,
+            progress: Optional[Callable[[int], None]] = None):
+        """Execute iterations until `iterations` or every replica is absorbed."""
+        stops = set()
+        if snapshots:
+            stops |= {i for i in SNAPSHOT_ITERS if i <= self.T}
+        if png:
+            stops |= {i + 1 for i in PNG_ITERS if i + 1 <= self.T + 1}
+        while self.t <= self.T:
+            if self.t in stops:
+                self._capture(self.t, snapshots and self.t in SNAPSHOT_ITERS,
+                              png and (self.t - 1) in PNG_ITERS)
+            nxt = min([s for s in stops if s > self.t] + [self.t + chunk, self.T + 1])
+            self.step(nxt - self.t)
+            if progress:
+                progress(self.t - 1)
+            if self.all_stopped():
+                break
+        if png and self.t in stops and (self.t - 1) in PNG_ITERS:
+            self._capture(self.t, False, True)
+        self.flush()
+        torch.cuda.synchronize(self.dev)
+        self.stopped = self.stop_iter.cpu().numpy().astype(np.int64)
+
+    def _capture(self, t, snap, png):
+        """Host copies of S_t / R_t at iteration start (spgg.py:397-402) and of the
+        strategies after iteration t-1 for the PNG snapshot (spgg.py:553-559)."""
+        stop = self.stop_iter.cpu().numpy()
+        cur = (t - 1) & 1
+        S = self.S[cur].cpu().numpy()
+        Rn = self.Rep[cur].cpu().numpy() if snap else None
+        for k in range(self.R):
+            if stop[k] != 0:
+                continue
+            if snap:
+                self.snapshots[k][t] = (Rn[k].reshape(self.L, self.L).copy(),
+                                        S[k].reshape(self.L, self.L).astype(np.int64))
+            if png:
+                self.png_frames[k][t - 1] = S[k].reshape(self.L, self.L).astype(np.int64)
+
+    # -- results -------------------------------------------------------------
+    def last_iteration(self, k) -> int:
+        """Iterations with a start record (incl. the absorbing one)."""
+        s = int(self.stopped[k])
+        return s if s else self.t - 1
+
+    def final_state(self, k):
+        """(Q (L,L,2,2), R (L,L), S (L,L) int64) of replica k after the run."""
+        last = self.last_iteration(k)
+        s = int(self.stopped[k])
+        cur = (last - 1) & 1 if s else last & 1   # S_{last} if absorbed, else S_{last+1}
+        L = self.L
+        Q = self.Q[k].cpu().numpy().reshape(L, L, 2, 2)
+        R = self.Rep[cur, k].cpu().numpy().reshape(L, L)
+        S = self.S[cur, k].cpu().numpy().reshape(L, L).astype(np.int64)
+        return Q, R, S
+
+    def payoff_at(self, t):
+        """P from S_t for every replica (device kernel), as (R, L, L) float64."""
+        C.check(self.lib.spgg_payoff(self.ctx, int(t), self.P_buf.data_ptr(), self.stream),
+                self.ctx, "spgg_payoff")
+        return self.P_buf.cpu().numpy().reshape(self.R, self.L, self.L)
+
+    def mt_state_host(self, k):
+        st = self.mt_state[k].cpu().numpy().view(np.uint32)
+        return st[:624].copy(), int(st[624])
+
+    def histories(self):
+        """Per-replica dict of the reference's per-iteration datasets (spgg.py:595-618)."""
+        st = self.stats.cpu().numpy()
+        return [histories_from_stats(st[k], self.last_iteration(k), int(self.stopped[k]) != 0,
+                                     self.eps_host[k], self.n) for k in range(self.R)]
+
+    def gmax_history(self, k):
+        st = self.stats[k, :, C.ST_GMAX].cpu().numpy()
+        last = self.last_iteration(k)
+        m = last - 1 if int(self.stopped[k]) else last
+        return st[1:m + 1]
+
+
+_STEP_KEYS = (
+    ["switch_C_to_D", "switch_D_to_C", "neighbor_influence_percent",
+     "payoff_component_history", "rep_component_history",
+     "best_neighbor_second_order_percent", "reputation_reward_ratio",
+     "avg_reward_C_history", "avg_reward_D_history"]
+    + [f"group_comp_d{d}_history" for d in range(6)]
+    + [f"{g}_q_{s}_{a}_history" for g in ("cooperators", "defectors")
+       for s in ("s0", "s1") for a in ("c", "d")]
+    + [f"avg_q_{s}_{a}_history" for s in ("s0", "s1") for a in ("c", "d")]
+)
+
+
+def histories_from_stats(S, last, stopped, eps_row, n):
+    """Turn one replica's device history record into the reference's datasets.
+
+    S: (iterations+2, NSTAT) float64 record; last: iterations with a start
+    record (incl. an absorbing one); stopped: absorbed at `last`; eps_row: eps
+    table (eps_row[t] = eps used by iteration t).  Means are sum/count, as
+    np.mean (spgg.py:383-394, 419-426, 511-592); empty masks give the
+    reference's 0 / NaN.
+    """
+    n = float(n)
+    m = last - 1 if stopped else last
+    it = S[1:last + 1]
+    nc = it[:, C.ST_NCOOP]
+    nd = n - nc
+    ds = {}
+    ds["coop_rate_history"] = nc / n
+    sump = it[:, C.ST_SUMP]
+    ds["it_records_final"] = np.stack([
+        nc / n, nd / n, sump, sump / n,
+        np.where(nc > 0, it[:, C.ST_SUMP_C] / np.maximum(nc, 1), 0.0),
+        np.where(nd > 0, it[:, C.ST_SUMP_D] / np.maximum(nd, 1), 0.0)], axis=1).reshape(-1, 6)
+    ds["rep_avg_history_final"] = it[:, C.ST_SUMR] / n
+    if m == 0:
+        empty = np.array([])
+        for key in _STEP_KEYS:
+            ds[key] = empty
+        ds["epsilon_history_final"] = empty
+        return ds
+    st_m = S[1:m + 1]
+    nc_m = st_m[:, C.ST_NCOOP]            # prev_S == 0 count of step i
+    nc_d = n - nc_m
+    na_c = S[2:m + 2, C.ST_NCOOP]         # a == 0 count of step i
+    na_d = n - na_c
+    ds["epsilon_history_final"] = np.array(eps_row[2:m + 2], dtype=np.float64)
+    ds["switch_C_to_D"] = st_m[:, C.ST_SW_CD].astype(np.int64)
+    ds["switch_D_to_C"] = st_m[:, C.ST_SW_DC].astype(np.int64)
+    ds["neighbor_influence_percent"] = st_m[:, C.ST_SUM_PCT] / n
+    ds["payoff_component_history"] = st_m[:, C.ST_SUM_WPP] / n
+    ds["rep_component_history"] = st_m[:, C.ST_SUM_WRR] / n
+    npos = st_m[:, C.ST_NMD_POS]
+    ds["best_neighbor_second_order_percent"] = np.where(
+        npos > 0, st_m[:, C.ST_NMD_POS2] / np.maximum(npos, 1) * 100, 0.0)
+    ds["reputation_reward_ratio"] = np.where(
+        na_c > 0, st_m[:, C.ST_SUM_RATIO_C] / np.maximum(na_c, 1), np.nan)
+    ds["avg_reward_C_history"] = np.where(na_c > 0, st_m[:, C.ST_SUM_REW_C] / np.maximum(na_c, 1), 0.0)
+    ds["avg_reward_D_history"] = np.where(na_d > 0, st_m[:, C.ST_SUM_REW_D] / np.maximum(na_d, 1), 0.0)
+    for d in range(6):
+        ds[f"group_comp_d{d}_history"] = (st_m[:, C.ST_GC0 + d] / n) * 100
+    for s_i, s_n in enumerate(("s0", "s1")):
+        for a_i, a_n in enumerate(("c", "d")):
+            e = 2 * s_i + a_i
+            ds[f"cooperators_q_{s_n}_{a_n}_history"] = np.where(
+                nc_m > 0, st_m[:, C.ST_SUMQ_C + e] / np.maximum(nc_m, 1), np.nan)
+            ds[f"defectors_q_{s_n}_{a_n}_history"] = np.where(
+                nc_d > 0, st_m[:, C.ST_SUMQ_D + e] / np.maximum(nc_d, 1), np.nan)
+            ds[f"avg_q_{s_n}_{a_n}_history"] = st_m[:, C.ST_SUMQ + e] / n
+    return ds

@@ -1,0 +1,166 @@
+"""HIP path vs the reference (golden fixtures) and the oracle — runs on the MI355X box.
+
+Bar: bit-exact for S, R, Q, counts and every deterministic dataset; float
+diagnostics reduced on the device (sums in a different order than np.mean's
+pairwise sum) within rtol 1e-5 (north_star tolerance)."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import spgg_amd  # noqa: E402
+from spgg_amd.engine import BatchEngine, ReplicaParams, reference_init  # noqa: E402
+from spgg_amd.h5io import read_datasets  # noqa: E402
+from oracle import spgg_oracle as O  # noqa: E402
+from tests._golden import Case, case_names  # noqa: E402
+
+FLOAT_TOL = dict(rtol=1e-5, atol=1e-9)
+APPROX = {"it_records_final", "rep_avg_history_final", "neighbor_influence_percent",
+          "payoff_component_history", "rep_component_history", "reputation_reward_ratio",
+          "avg_reward_C_history", "avg_reward_D_history"} | {
+    f"{g}_q_{s}_{a}_history" for g in ("cooperators", "defectors", "avg")
+    for s in ("s0", "s1") for a in ("c", "d")}
+
+
+def _pinned_model(c):
+    orig = np.random.seed
+    np.random.seed = lambda s=None: orig(c.seed if s is None else s)
+    try:
+        kw = dict(c.kwargs)
+        if c.S_in_one is not None:
+            kw["S_in_one"] = c.S_in_one
+        if c.algorithm_instance:
+            kw["algorithm"] = spgg_amd.QLearning(**c.algorithm_instance)
+        return spgg_amd.SPGG(**kw)
+    finally:
+        np.random.seed = orig
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_spgg_dropin_matches_reference(name, tmp_path):
+    c = Case(name)
+    m = _pinned_model(c)
+    m.save_png = False
+    m.folder = str(tmp_path)
+    fn = str(tmp_path / "experiment_data.h5")
+    ret = m.run(fn)
+    got = read_datasets(fn)
+    assert set(got) == set(c.datasets), sorted(set(got) ^ set(c.datasets))
+    for k, w in c.datasets.items():
+        g = got[k]
+        assert g.shape == w.shape, (k, g.shape, w.shape)
+        if k in APPROX:
+            np.testing.assert_allclose(g, w, equal_nan=True, err_msg=k, **FLOAT_TOL)
+        else:
+            assert np.array_equal(g, w, equal_nan=w.dtype.kind == "f"), k
+    assert np.array_equal(m.q_table, c.q_table)
+    assert np.array_equal(m.R, c.R)
+    assert np.array_equal(m._Sn, c.Sn)
+    assert np.array_equal(np.array(ret, dtype=float), c.ret)
+    assert m.algorithm.epsilon == c.epsilon
+
+
+def _oracle_final(L, T, p, seed, M2, state):
+    op = O.Params(L=L, iterations=T, use_second_order=M2, state_representation=state,
+                  **{k: getattr(p, k) for k in ("r", "c", "cost", "alpha", "gamma", "epsilon",
+                                                 "epsilon_decay", "epsilon_min", "influence_factor",
+                                                 "lambda_epsilon", "delta_R_D", "R_min", "R_max",
+                                                 "reward_weight_payoff", "rep_gain_C")})
+    ds, fin = O.run(op, np.random.RandomState(seed), collect_snapshots=False)
+    return ds, fin
+
+
+def _runner_params(**kw):
+    base = dict(c=1, cost=1, alpha=0.8, gamma=0.9, epsilon=0.5, epsilon_decay=0.99,
+                epsilon_min=0.01, lambda_epsilon=0.01, delta_R_D=1, R_min=-10, R_max=10,
+                rep_gain_C=1.0, reward_weight_payoff=0.95, influence_factor=1.0, r=3.0)
+    base.update(kw)
+    return ReplicaParams(**base)
+
+
+@pytest.mark.parametrize("M2,state", [(False, "reputation"), (True, "action"), (True, "reputation")])
+def test_batched_replicas_match_oracle(M2, state):
+    L, T = 20, 60
+    reps = [_runner_params(r=r, influence_factor=k, seed=s)
+            for r, k, s in [(2.5, 0.0, 1), (3.0, 1.0, 2), (3.8, 0.5, 3), (5.0, 2.0, 4), (1.0, 1.0, 5)]]
+    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng="mt19937")
+    eng.run(snapshots=False)
+    hs = eng.histories()
+    for k, p in enumerate(reps):
+        ds, fin = _oracle_final(L, T, p, p.seed, M2, state)
+        Q, R, S = eng.final_state(k)
+        assert np.array_equal(Q, fin["Q"]), k
+        assert np.array_equal(R, fin["R"]), k
+        assert np.array_equal(S, fin["S"]), k
+        assert np.array_equal(hs[k]["coop_rate_history"], ds["coop_rate_history"]), k
+        assert np.array_equal(hs[k]["switch_C_to_D"], ds["switch_C_to_D"]) or ds["switch_C_to_D"].size == 0
+    eng.close()
+
+
+def test_device_mt19937_equals_host_injection():
+    L, T = 24, 40
+    reps = [_runner_params(seed=s) for s in (10, 11, 12)]
+    outs = []
+    for rng in ("mt19937", "inject"):
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng)
+        eng.run(snapshots=False)
+        outs.append([eng.final_state(k) for k in range(len(reps))])
+        eng.close()
+    for a, b in zip(*outs):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
+def test_device_mt_stream_matches_numpy():
+    """spgg_draw: the device key reproduces RandomState.rand/randint bytes exactly."""
+    L, T = 37, 3   # 3*37^2 words: several key blocks with a straddling pair
+    reps = [_runner_params(seed=7, epsilon=0.5)]
+    eng = BatchEngine(L, T, reps, use_second_order=False, rng="mt19937")
+    rs = np.random.RandomState(7)
+    rs.uniform(-0.01, 0.01, (L, L, 2, 2)); rs.randint(0, 2, (L, L))
+    lib = eng.lib
+    for t in (1, 2, 3):
+        from spgg_amd import _lib as C
+        C.check(lib.spgg_draw(eng.ctx, t, eng.stream), eng.ctx, "spgg_draw")
+        u = rs.rand(L, L).reshape(-1)
+        b = rs.randint(0, 2, (L, L)).reshape(-1)
+        assert np.array_equal(eng.explore[0].cpu().numpy(), (u < eng.eps_host[0, t]).astype(np.uint8))
+        assert np.array_equal(eng.rbit[0].cpu().numpy(), b.astype(np.uint8))
+    eng.close()
+
+
+@pytest.mark.parametrize("L,T,M2", [(200, 150, False), (200, 60, True), (1000, 3, False)])
+def test_full_size_bit_exact(L, T, M2):
+    p = _runner_params(seed=0)
+    eng = BatchEngine(L, T, [p], use_second_order=M2, rng="mt19937")
+    eng.run(snapshots=False)
+    ds, fin = _oracle_final(L, T, p, 0, M2, "reputation")
+    Q, R, S = eng.final_state(0)
+    assert np.array_equal(S, fin["S"]) and np.array_equal(R, fin["R"]) and np.array_equal(Q, fin["Q"])
+    h = eng.histories()[0]
+    assert np.array_equal(h["coop_rate_history"], ds["coop_rate_history"])
+    np.testing.assert_allclose(h["neighbor_influence_percent"], ds["neighbor_influence_percent"], **FLOAT_TOL)
+    eng.close()
+
+
+def test_philox_mode_deterministic_and_sane():
+    L, T = 64, 300
+    reps = [_runner_params(seed=s) for s in range(4)]
+    res = []
+    for _ in range(2):
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng="philox")
+        eng.run(snapshots=False)
+        res.append([eng.final_state(k) for k in range(4)])
+        hs = eng.histories()
+        eng.close()
+    for a, b in zip(*res):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    for h in hs:
+        cr = h["coop_rate_history"]
+        assert np.all((cr >= 0) & (cr <= 1))
+        # identical eps schedule to the reference
+        assert h["epsilon_history_final"][0] == max(0.5 * 0.99, 0.01)

@@ -122,8 +122,9 @@ def test_device_mt_stream_matches_numpy():
     rs = np.random.RandomState(7)
     rs.uniform(-0.01, 0.01, (L, L, 2, 2)); rs.randint(0, 2, (L, L))
     lib = eng.lib
+    from spgg_amd import _lib as C
+    eng.stats[:, :, C.ST_NCOOP] = 1.0   # no iteration is absorbing: every draw happens
     for t in (1, 2, 3):
-        from spgg_amd import _lib as C
         C.check(lib.spgg_draw(eng.ctx, t, eng.stream), eng.ctx, "spgg_draw")
         u = rs.rand(L, L).reshape(-1)
         b = rs.randint(0, 2, (L, L)).reshape(-1)

@@ -16,6 +16,8 @@
  *
  * Conventions: every function returns 0 on success, a negative SPGG_E* code on
  * failure (detail in spgg_last_error).  No C++ exception crosses the ABI.
+ * One iteration is ONE kernel launch over all replicas (plus one MT19937 draw
+ * launch in that mode).
  * Buffers are DEVICE pointers owned by the caller (e.g. torch tensors); the
  * library only allocates its per-replica parameter table and frees it in
  * spgg_destroy.  A context is bound to one device and is not thread-safe.
@@ -30,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 1
+#define SPGG_ABI_VERSION 2
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -106,16 +108,24 @@ typedef struct {
   double r_max;
   uint64_t seed;      /* Philox key (SPGG_RNG_PHILOX only) */
   uint64_t reserved;
+  /* group payoff of a cooperator / defector in a group with N cooperators,
+   * N = 0..5: (r*c*N)/5 - cost and (r*c*N)/5 (spgg.py:256-257), computed by
+   * the host in the reference's order. */
+  double pay_c[6];
+  double pay_d[6];
 } spgg_rep_params;
 
-/* Device buffers, all replica-major.  n = L*L.
- *   S[2]      uint8  [n_rep][n]      strategy ping-pong, S_t lives in S[(t-1)&1]
- *   R[2]      f64    [n_rep][n]      reputation ping-pong, R_t in R[(t-1)&1]
- *   Q         f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2)
- *   reward    f64    [n_rep][n]      scratch: reward of the current step
- *   aux       uint8  [n_rep][n]      scratch: s_old | prevS<<1 | (a*==a)<<2
- *   ni_md     f64    [n_rep][n]      pending NI: max(0, max_diff)
- *   ni_atd    f64    [n_rep][n]      pending NI: |alpha*td'| (diagnostic)
+/* Device buffers, all replica-major.  n = L*L.  Ping-pong pairs are indexed
+ * by iteration parity: iteration t reads [ (t-1)&1 ] and writes [ t&1 ].
+ *   S[2]      uint8  [n_rep][n]      bit0: strategy S_t (0 = C); bits 1-3: the
+ *                                    deferred-NI record of iteration t-1
+ *                                    (s_old, a*==a, prev strategy)
+ *   R[2]      f64    [n_rep][n]      reputation R_t
+ *   Q[2]      f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2);
+ *                                    Q[(t-1)&1] holds iteration t-1's TD update
+ *                                    without its NI term (applied by iteration t)
+ *   md[2]     f64    [n_rep][n]      max(0, max_diff) of iteration t-1
+ *   atd       f32    [n_rep][n]      |alpha*td'| of the pending iteration (diagnostic)
  *   explore   uint8  [n_rep][n]      eps-greedy explore flag of the step (INJECT/MT19937)
  *   rbit      uint8  [n_rep][n]      random action of the step          (INJECT/MT19937)
  *   mt_state  uint32 [n_rep][625]    MT19937 key[624] + pos (MT19937 only)
@@ -123,15 +133,17 @@ typedef struct {
  *   stats     f64    [n_rep][iterations+2][SPGG_NSTAT]  zero-initialised; slot
  *                                    t0 must hold NCOOP of S_t0 before stepping
  *   stop_iter int32  [n_rep]         0 while running, else the absorbing iteration
+ * Initial state: S[0] = population (bits 1-3 zero), R[0] = 0, Q[0] = initial table.
+ * Final state of a replica absorbed at s: S,R in [(s-1)&1], Q in [s&1]; of a
+ * replica still running after spgg_flush(t_last): S,R in [t_last&1], Q in
+ * [(t_last+1)&1].
  */
 typedef struct {
   uint8_t* S[2];
   double* R[2];
-  double* Q;
-  double* reward;
-  uint8_t* aux;
-  double* ni_md;
-  double* ni_atd;
+  double* Q[2];
+  double* md[2];
+  float* atd;
   uint8_t* explore;
   uint8_t* rbit;
   uint32_t* mt_state;
@@ -164,6 +176,9 @@ int spgg_draw(spgg_ctx* ctx, int32_t t, void* hip_stream);
 /* P (normalised payoff, spgg.py:373-378) of every agent from S_t into
  * out[n_rep][n] (device).  Used for SPGG.P and run()'s return value. */
 int spgg_payoff(spgg_ctx* ctx, int32_t t, double* out, void* hip_stream);
+
+/* Tile shape (agents) the step kernel uses for this lattice. */
+int spgg_tile_shape(const spgg_ctx* ctx, int32_t* tw, int32_t* th);
 
 int spgg_destroy(spgg_ctx* ctx);
 

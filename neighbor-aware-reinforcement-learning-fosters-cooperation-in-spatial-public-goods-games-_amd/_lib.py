@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -28,7 +28,8 @@ ST_SUMQ, ST_SUMQ_C, ST_SUMQ_D, ST_GMAX = 21, 25, 29, 33
 NSTAT = 34
 
 EXPORTED = ("spgg_abi_version", "spgg_last_error", "spgg_create", "spgg_set_params",
-            "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_destroy")
+            "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
+            "spgg_destroy")
 
 
 class Config(ctypes.Structure):
@@ -42,15 +43,15 @@ class RepParams(ctypes.Structure):
     _fields_ = [(name, ctypes.c_double) for name in (
         "rc", "cost", "norm_min", "norm_den", "w_p", "w_rep", "alpha", "gamma",
         "diag_alpha", "diag_gamma", "kappa", "lambda_eps", "rep_gain_c", "neg_delta_r_d",
-        "r_min", "r_max")] + [("seed", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+        "r_min", "r_max")] + [("seed", ctypes.c_uint64), ("reserved", ctypes.c_uint64),
+                              ("pay_c", ctypes.c_double * 6), ("pay_d", ctypes.c_double * 6)]
 
 
 class Buffers(ctypes.Structure):
-    _fields_ = [("S", ctypes.c_void_p * 2), ("R", ctypes.c_void_p * 2), ("Q", ctypes.c_void_p),
-                ("reward", ctypes.c_void_p), ("aux", ctypes.c_void_p), ("ni_md", ctypes.c_void_p),
-                ("ni_atd", ctypes.c_void_p), ("explore", ctypes.c_void_p), ("rbit", ctypes.c_void_p),
-                ("mt_state", ctypes.c_void_p), ("eps", ctypes.c_void_p), ("stats", ctypes.c_void_p),
-                ("stop_iter", ctypes.c_void_p)]
+    _fields_ = [("S", ctypes.c_void_p * 2), ("R", ctypes.c_void_p * 2), ("Q", ctypes.c_void_p * 2),
+                ("md", ctypes.c_void_p * 2), ("atd", ctypes.c_void_p), ("explore", ctypes.c_void_p),
+                ("rbit", ctypes.c_void_p), ("mt_state", ctypes.c_void_p), ("eps", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p), ("stop_iter", ctypes.c_void_p)]
 
 
 class SpggError(RuntimeError):
@@ -90,6 +91,8 @@ def load(path: str | None = None):
         lib.spgg_draw.argtypes = [vp, i32, vp]
         lib.spgg_payoff.restype = ctypes.c_int
         lib.spgg_payoff.argtypes = [vp, i32, vp, vp]
+        lib.spgg_tile_shape.restype = ctypes.c_int
+        lib.spgg_tile_shape.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         lib.spgg_destroy.restype = ctypes.c_int
         lib.spgg_destroy.argtypes = [vp]
         v = lib.spgg_abi_version()

@@ -25,7 +25,7 @@ def needs_build(out=OUT):
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    deps = SRC + [os.path.join(INC, "spgg_abi.h")]
+    deps = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

@@ -1,0 +1,155 @@
+// spgg_device.h — device helpers shared by the SPGG kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "spgg_abi.h"
+
+namespace spgg {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ int wrap(int x, int L) {
+  while (x < 0) x += L;
+  while (x >= L) x -= L;
+  return x;
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup reduction of K per-thread f64 partials (K a power of two <= 64).
+// Butterfly "transpose" reduce: at each xor level a lane keeps one half of its
+// values and ships the other half, so K values cost ~K shuffles instead of
+// 6K.  Afterwards lane l holds the wave sum of value (l >> log2(64/K)).
+template <int CNT, int MASK, int K>
+__device__ __forceinline__ void transpose_level(double (&v)[K], int lane) {
+  if constexpr (MASK >= 1) {
+    if constexpr (CNT > 1) {
+      constexpr int h = CNT / 2;
+      const bool upper = (lane & MASK) != 0;
+#pragma unroll
+      for (int i = 0; i < h; ++i) {
+        const double send = upper ? v[i] : v[i + h];
+        const double keep = upper ? v[i + h] : v[i];
+        v[i] = keep + __shfl_xor(send, MASK);
+      }
+      transpose_level<h, MASK / 2, K>(v, lane);
+    } else {
+      v[0] += __shfl_xor(v[0], MASK);
+      transpose_level<1, MASK / 2, K>(v, lane);
+    }
+  }
+}
+
+// Reduce v over the workgroup; thread k < K then returns the total of value k.
+// lds must hold kWaves*K doubles.
+template <int K>
+__device__ __forceinline__ double block_reduce(double (&v)[K], double* lds) {
+  static_assert(K >= 1 && K <= 64 && (K & (K - 1)) == 0, "K must be a power of two");
+  transpose_level<K, 32, K>(v, threadIdx.x & 63);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int per = 64 / K;
+  if ((lane & (per - 1)) == 0) lds[wave * K + lane / per] = v[0];
+  __syncthreads();
+  double tot = 0.0;
+  if (threadIdx.x < K) {
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tot += lds[w * K + threadIdx.x];
+  }
+  return tot;
+}
+
+// Max of non-negative v over the workgroup, valid in thread 0.  lds: kWaves doubles.
+__device__ __forceinline__ double block_reduce_max(double v, double* lds) {
+#pragma unroll
+  for (int mask = 32; mask >= 1; mask >>= 1) v = fmax(v, __shfl_xor(v, mask));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  double m = 0.0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) m = fmax(m, lds[w]);
+  }
+  return m;
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (counter-based): performance-mode eps-greedy draws, keyed by
+// the replica seed, counter (agent, iteration, replica, tag).
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+  }
+  return c;
+}
+
+// numpy legacy random_sample: 53-bit double from two 32-bit words.
+__device__ __forceinline__ double mt_double(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
+
+// eps-greedy draw of agent `idx` at iteration t (Philox mode): explore flag + random action.
+__device__ __forceinline__ void philox_draw(int idx, int t, int rep, uint64_t seed, double eps,
+                                            int* explore, int* rbit) {
+  const uint4 w = philox4x32_10(make_uint4((uint32_t)idx, (uint32_t)t, (uint32_t)rep, 0x53504747u),
+                                (uint32_t)seed, (uint32_t)(seed >> 32));
+  *explore = mt_double(w.x, w.y) < eps ? 1 : 0;  // algorithms.py:105
+  *rbit = (int)(w.z & 1u);                        // algorithms.py:108
+}
+
+// q[4] accessors with a run-time index, kept in registers (no scratch).
+__device__ __forceinline__ double q_get(const double (&q)[4], int e) {
+  return e == 0 ? q[0] : (e == 1 ? q[1] : (e == 2 ? q[2] : q[3]));
+}
+__device__ __forceinline__ void q_set(double (&q)[4], int e, double x) {
+  q[0] = e == 0 ? x : q[0];
+  q[1] = e == 1 ? x : q[1];
+  q[2] = e == 2 ? x : q[2];
+  q[3] = e == 3 ? x : q[3];
+}
+
+// Reputation state threshold: (acc / n) > 0  <=>  acc >= k * 2^-1074 with
+// k = 3 (n = 5) or 7 (n = 13): the smallest sums whose quotient does not
+// round to zero.  Exact for every double acc, no division (spgg.py:306-307).
+__device__ __forceinline__ double rep_threshold(bool m2) {
+  return __longlong_as_double(m2 ? 7LL : 3LL);  // 7*2^-1074 / 3*2^-1074 (subnormals)
+}
+
+// ---------------------------------------------------------------------------
+// Payoff of one agent given the cooperator indicators of the 13 cells around
+// it (spgg.py:230-259, 373-377): group counts N_k at the centre and the four
+// axial neighbours, P_k = S0 ? (r*c*N_k)/5 - cost : (r*c*N_k)/5 (table lookups
+// with host-computed entries, equal in value to the reference's
+// (t-cost)*S0 + t*S1), summed in the reference's group order, normalised.
+struct Cells13 {
+  int c00, cm0, cp0, c0m, c0p, cmm, cmp, cpm, cpp, cM0, cP0, c0M, c0P;
+};
+
+// tab: LDS copy of pay_c[6] followed by pay_d[6].
+__device__ __forceinline__ double payoff13(const Cells13& c, const double* tab, double norm_min,
+                                           double norm_den) {
+  const int N0 = c.c00 + c.cm0 + c.cp0 + c.c0m + c.c0p;  // group (0,0)  -> N0[i,j]
+  const int N1 = c.cm0 + c.cM0 + c.c00 + c.cmm + c.cmp;  // group (1,0)  -> N0[i-1,j]
+  const int N2 = c.cp0 + c.c00 + c.cP0 + c.cpm + c.cpp;  // group (-1,0) -> N0[i+1,j]
+  const int N3 = c.c0m + c.cmm + c.cpm + c.c0M + c.c00;  // group (1,1)  -> N0[i,j-1]
+  const int N4 = c.c0p + c.cmp + c.cpp + c.c00 + c.c0P;  // group (-1,1) -> N0[i,j+1]
+  const double* t = tab + (c.c00 ? 0 : 6);
+  double tot = t[N0];
+  tot = tot + t[N1];
+  tot = tot + t[N2];
+  tot = tot + t[N3];
+  tot = tot + t[N4];
+  return (tot - norm_min) / norm_den;
+}
+
+}  // namespace spgg

@@ -1,486 +1,501 @@
 // spgg_kernels.hip — MI355X (gfx950) kernels for the SPGG per-iteration hot path.
 //
-// One iteration t of the reference's run loop (src/model/spgg.py:368-592) is
-// two launches over every replica in the batch:
+// ONE launch per iteration t of the reference's run loop
+// (src/model/spgg.py:368-592) covers every replica of the batch.  A
+// workgroup owns a TH x TW tile of one replica's periodic L x L lattice:
 //
-//   act(t)   per agent: [finalize the deferred neighbor-influence (NI) term of
-//            iteration t-1 + its Q statistics] -> payoff P from S_t (13-cell
-//            stencil) -> iteration-start record -> absorbing-stop check ->
-//            state s from R_t -> eps-greedy action -> R_{t+1}, S_{t+1}, reward
-//   learn(t) per agent: state s' from R_{t+1} -> Q-learning TD update ->
-//            diagnostic TD -> NI max/argmax over the 4 (M=1) / 12 (M=2)
-//            neighbor rewards -> pending NI record + lattice-wide max |diff|
+//   phase 0  stage S_t (halo M+2) and R_t (halo 2M) of the tile in LDS; load
+//            the owned agents' Q and pending neighbor-influence (NI) record
+//   phase 1  owned agents: apply the deferred NI term of iteration t-1
+//            (+ its Q statistics) -> payoff P (13-cell stencil) -> iteration
+//            start record -> absorbing-stop check -> state s from R_t ->
+//            eps-greedy action -> R_{t+1}, reward.  The ring of neighbours at
+//            distance <= M (owned by other workgroups) is recomputed the same
+//            way, so every reward/action the tile's NI needs is in LDS.
+//   phase 2  owned agents: s' from R_{t+1} -> Q-learning TD -> diagnostic TD
+//            -> NI max/argmax over 4 (M=1) / 12 (M=2) neighbour rewards ->
+//            pending NI record, lattice-wide max |diff| (atomic), S_{t+1}.
 //
-// The NI term divides by the lattice-wide max (spgg.py:488), so it cannot be
-// applied in the pass that produces the rewards; it is applied by the NEXT
-// act launch (or spgg_flush), reproducing the reference's arithmetic exactly:
+// The NI term divides by a lattice-wide max (spgg.py:488), so it is applied
+// one launch later (or by spgg_flush) with the reference's exact arithmetic:
 //   Q[s,a] = (qc + alpha*td) + (kappa*max(0,md))/(gmax+lambda_eps) * (+-1).
+// Q and the pending max_diff are ping-ponged by iteration parity: a launch
+// reads only buffers the previous launch wrote, so the ring recompute never
+// races another workgroup's writes.
 //
-// Every float op is f64 and written in the reference's evaluation order; the
-// file is compiled with -ffp-contract=off so no FMA contraction changes a bit.
-// Per-step history values are reduced per workgroup (wave butterfly +
-// LDS) and added with one f64 atomic per value per workgroup.
+// Every float op that feeds the simulation is f64 in the reference's
+// evaluation order; compiled with -ffp-contract=off (no FMA contraction).
+// History values are reduced per workgroup (wave butterfly + LDS) and added
+// with one f64 atomic per value per workgroup.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
 
 #include "spgg_abi.h"
+#include "spgg_device.h"
+
+using namespace spgg;
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
 constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
 
-struct KArgs {
-  const uint8_t* S_cur;  // S_t
-  uint8_t* S_nxt;        // S_{t+1}
-  const double* R_cur;   // R_t
-  double* R_nxt;         // R_{t+1}
-  double* Q;             // [rep][n][4]
-  double* reward;
-  uint8_t* aux;
-  double* ni_md;
-  double* ni_atd;
+struct TileArgs {
+  const uint8_t* S_in;  // S_t   (bit0 strategy, bits1-3 pending-NI bookkeeping)
+  uint8_t* S_out;       // S_{t+1}
+  const double* R_in;
+  double* R_out;
+  const double* Q_in;   // [rep][n][4]: after TD of t-1, before its NI term
+  double* Q_out;
+  const double* md_in;  // max(0, max_diff) of t-1
+  double* md_out;
+  float* atd;           // |alpha*td'| of the pending iteration (owner only)
   const uint8_t* explore;
   const uint8_t* rbit;
   const double* eps;
   double* stats;
   int* stop_iter;
   const spgg_rep_params* params;
-  int L;
-  int n;
-  int chunk;  // agents per workgroup
-  int slots;  // iterations + 2
+  int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
 };
 
-__device__ __forceinline__ int wrap(int x, int L) {
-  while (x < 0) x += L;
-  while (x >= L) x -= L;
-  return x;
+// Value slots of the workgroup reductions.
+enum { F_PCT = 0, F_Q = 1, F_QC = 5, F_QD = 9, F_N = 13 };  // -> slot t-1
+enum {
+  A_SUMP = 0, A_SUMP_C, A_SUMP_D, A_SUMR,                   // -> slot t
+  A_SWCD, A_SWDC, A_WPP, A_WRR, A_REWC, A_REWD, A_RATIO,    // -> slot t
+  A_NCOOP1,                                                 // -> slot t+1
+  A_N
+};
+enum { L_GC = 0, L_NMD = 6, L_NMD2 = 7, L_N = 8 };           // -> slot t
+
+struct LdsLayout {
+  int sw, sh, rw, rh, aw, ah;
+  int off_R, off_Rn, off_Rew, off_S, off_A, bytes;
+};
+
+// f64 arrays first (16-byte aligned carve), then bytes.
+__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HR, int HA) {
+  LdsLayout l;
+  l.sw = tw + 2 * HS; l.sh = th + 2 * HS;
+  l.rw = tw + 2 * HR; l.rh = th + 2 * HR;
+  l.aw = tw + 2 * HA; l.ah = th + 2 * HA;
+  int off = (12 + kWaves * 64) * 8;  // payoff table + reduction scratch
+  l.off_R = off;   off += ((l.rw * l.rh * 8 + 15) / 16) * 16;
+  l.off_Rn = off;  off += ((l.aw * l.ah * 8 + 15) / 16) * 16;
+  l.off_Rew = off; off += ((l.aw * l.ah * 8 + 15) / 16) * 16;
+  l.off_S = off;   off += ((l.sw * l.sh + 15) / 16) * 16;
+  l.off_A = off;   off += ((l.aw * l.ah + 15) / 16) * 16;
+  l.bytes = off;
+  return l;
 }
 
-// ---------------------------------------------------------------------------
-// Workgroup reduction of K per-thread f64 partials (K a power of two <= 64).
-// Butterfly "transpose" reduce: at each xor level a lane keeps one half of its
-// values and ships the other half, so K values cost ~K shuffles instead of
-// 6K.  Afterwards lane l holds the wave sum of value (l >> log2(64/K)).
-template <int CNT, int MASK, int K>
-__device__ __forceinline__ void transpose_level(double (&v)[K], int lane) {
-  if constexpr (MASK >= 1) {
-    if constexpr (CNT > 1) {
-      constexpr int h = CNT / 2;
-      const bool upper = (lane & MASK) != 0;
-#pragma unroll
-      for (int i = 0; i < h; ++i) {
-        const double send = upper ? v[i] : v[i + h];
-        const double keep = upper ? v[i + h] : v[i];
-        v[i] = keep + __shfl_xor(send, MASK);
-      }
-      transpose_level<h, MASK / 2, K>(v, lane);
-    } else {
-      v[0] += __shfl_xor(v[0], MASK);
-      transpose_level<1, MASK / 2, K>(v, lane);
-    }
+// Cooperator indicators of the 13 cells around centre index c of a byte grid
+// with row pitch w (bit0 = strategy, 0 = cooperate).
+__device__ __forceinline__ Cells13 cells_at(const uint8_t* s, int c, int w) {
+#define CO(o) ((s[c + (o)] & 1) ? 0 : 1)
+  Cells13 r;
+  r.c00 = CO(0);
+  r.cm0 = CO(-w); r.cp0 = CO(w); r.c0m = CO(-1); r.c0p = CO(1);
+  r.cmm = CO(-w - 1); r.cmp = CO(-w + 1); r.cpm = CO(w - 1); r.cpp = CO(w + 1);
+  r.cM0 = CO(-2 * w); r.cP0 = CO(2 * w); r.c0M = CO(-2); r.c0P = CO(2);
+#undef CO
+  return r;
+}
+
+// Reputation sum in the reference's offset order (spgg.py:296-305):
+// roll(R,(dx,dy))[i,j] = R[i-dx, j-dy]; acc starts at 0.0.
+template <bool M2>
+__device__ __forceinline__ int rep_state_lds(const double* R, int c, int w) {
+  double acc = 0.0;
+  acc += R[c];          // (0,0)
+  acc += R[c - w];      // (1,0)
+  acc += R[c + w];      // (-1,0)
+  acc += R[c - 1];      // (0,1)
+  acc += R[c + 1];      // (0,-1)
+  if constexpr (M2) {
+    acc += R[c - 2 * w];  // (2,0)
+    acc += R[c + 2 * w];  // (-2,0)
+    acc += R[c - 2];      // (0,2)
+    acc += R[c + 2];      // (0,-2)
+    acc += R[c - w - 1];  // (1,1)
+    acc += R[c - w + 1];  // (1,-1)
+    acc += R[c + w - 1];  // (-1,1)
+    acc += R[c + w + 1];  // (-1,-1)
   }
+  return acc >= rep_threshold(M2) ? 1 : 0;
+}
+
+// Deferred NI of iteration t-1 on one agent's Q (spgg.py:489-509).
+__device__ __forceinline__ double apply_pending(double (&q)[4], uint8_t b, double md, double kappa,
+                                                double lam_den) {
+  const int e = ((b >> 1) & 1) * 2 + (b & 1);  // (s_old, a) of iteration t-1
+  const double lam = (kappa * md) / lam_den;
+  const double nu = lam * (((b >> 2) & 1) ? 1.0 : -1.0);
+  q_set(q, e, q_get(q, e) + nu);
+  return nu;
 }
 
 template <int K>
-__device__ __forceinline__ double wave_transpose_reduce(double (&v)[K]) {
-  static_assert(K >= 1 && K <= 64 && (K & (K - 1)) == 0, "K must be a power of two");
+__device__ __forceinline__ void wave_partials(double (&v)[K], double* red, int base) {
   transpose_level<K, 32, K>(v, threadIdx.x & 63);
-  return v[0];
-}
-
-// q[4] accessors with a run-time index, kept in registers (no scratch).
-__device__ __forceinline__ double q_get(const double (&q)[4], int e) {
-  return e == 0 ? q[0] : (e == 1 ? q[1] : (e == 2 ? q[2] : q[3]));
-}
-__device__ __forceinline__ void q_set(double (&q)[4], int e, double x) {
-  q[0] = e == 0 ? x : q[0];
-  q[1] = e == 1 ? x : q[1];
-  q[2] = e == 2 ? x : q[2];
-  q[3] = e == 3 ? x : q[3];
-}
-
-// Reduce v over the workgroup; thread k < K then returns the total of value k.
-template <int K>
-__device__ __forceinline__ double block_reduce(double (&v)[K], double* lds) {
-  const double s = wave_transpose_reduce<K>(v);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int per = 64 / K;
-  if ((lane & (per - 1)) == 0) lds[wave * K + lane / per] = s;
-  __syncthreads();
-  double tot = 0.0;
-  if (threadIdx.x < K) {
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) tot += lds[w * K + threadIdx.x];
-  }
-  return tot;
+  if ((lane & (per - 1)) == 0) red[wave * 64 + base + lane / per] = v[0];
 }
 
-__device__ __forceinline__ double block_reduce_max(double v, double* lds) {
-#pragma unroll
-  for (int mask = 32; mask >= 1; mask >>= 1) v = fmax(v, __shfl_xor(v, mask));
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) lds[wave] = v;
-  __syncthreads();
-  double m = 0.0;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) m = fmax(m, lds[w]);
-  }
-  return m;
-}
+template <bool M2, bool AS, int RNG, int APT>
+__global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
+  constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
+  constexpr int HR = 2 * HA;      // R_t halo: states of ring agents
+  constexpr int HS = HA + 2;      // S_t halo: payoffs of ring agents
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-// ---------------------------------------------------------------------------
-// Philox4x32-10 (counter-based): performance-mode eps-greedy draws.
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
-  }
-  return c;
-}
-
-// numpy legacy random_sample: 53-bit double from two 32-bit words.
-__device__ __forceinline__ double mt_double(uint32_t a, uint32_t b) {
-  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
-}
-
-// ---------------------------------------------------------------------------
-// Payoff of agent (i,j) from S_t: 5 groups (spgg.py:373-377), each
-// P_k = ((r*c*N_k)/5 - cost)*S0 + ((r*c*N_k)/5)*S1 (spgg.py:256-257), with
-// N_k the cooperator count of the group centred at (i,j),(i-1,j),(i+1,j),
-// (i,j-1),(i,j+1) (group offsets read as (shift, axis), spgg.py:201).
-__device__ __forceinline__ double payoff(const uint8_t* S, int i, int j, int L,
-                                         const spgg_rep_params& p) {
-  const int im1 = wrap(i - 1, L), ip1 = wrap(i + 1, L), im2 = wrap(i - 2, L), ip2 = wrap(i + 2, L);
-  const int jm1 = wrap(j - 1, L), jp1 = wrap(j + 1, L), jm2 = wrap(j - 2, L), jp2 = wrap(j + 2, L);
-#define C0(r, c) (S[(r) * L + (c)] == 0 ? 1 : 0)
-  const int c_00 = C0(i, j), c_m0 = C0(im1, j), c_p0 = C0(ip1, j), c_0m = C0(i, jm1), c_0p = C0(i, jp1);
-  const int c_mm = C0(im1, jm1), c_mp = C0(im1, jp1), c_pm = C0(ip1, jm1), c_pp = C0(ip1, jp1);
-  const int c_M0 = C0(im2, j), c_P0 = C0(ip2, j), c_0M = C0(i, jm2), c_0P = C0(i, jp2);
-#undef C0
-  const int N[5] = {
-      c_00 + c_m0 + c_p0 + c_0m + c_0p,   // group (0,0)       -> N0[i,j]
-      c_m0 + c_M0 + c_00 + c_mm + c_mp,   // group (1,0)       -> N0[i-1,j]
-      c_p0 + c_00 + c_P0 + c_pm + c_pp,   // group (-1,0)      -> N0[i+1,j]
-      c_0m + c_mm + c_pm + c_0M + c_00,   // group (1,1)       -> N0[i,j-1]
-      c_0p + c_mp + c_pp + c_00 + c_0P};  // group (-1,1)      -> N0[i,j+1]
-  const double s0 = (double)c_00, s1 = (double)(1 - c_00);
-  double tot = 0.0;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const double tk = (p.rc * (double)N[k]) / 5.0;
-    const double pk = (tk - p.cost) * s0 + tk * s1;
-    tot = (k == 0) ? pk : tot + pk;
-  }
-  return (tot - p.norm_min) / p.norm_den;
-}
-
-// Reputation state (spgg.py:292-307): mean of R over 5 / 13 offsets > 0,
-// summed in the reference's offset order, starting from 0.0.
-template <bool M2>
-__device__ __forceinline__ int rep_state(const double* R, int i, int j, int L) {
-  const int im1 = wrap(i - 1, L), ip1 = wrap(i + 1, L);
-  const int jm1 = wrap(j - 1, L), jp1 = wrap(j + 1, L);
-  // roll(R, (dx,dy))[i,j] = R[i-dx, j-dy]
-  double acc = 0.0;
-  acc += R[i * L + j];      // (0,0)
-  acc += R[im1 * L + j];    // (1,0)
-  acc += R[ip1 * L + j];    // (-1,0)
-  acc += R[i * L + jm1];    // (0,1)
-  acc += R[i * L + jp1];    // (0,-1)
-  if constexpr (M2) {
-    const int im2 = wrap(i - 2, L), ip2 = wrap(i + 2, L);
-    const int jm2 = wrap(j - 2, L), jp2 = wrap(j + 2, L);
-    acc += R[im2 * L + j];    // (2,0)
-    acc += R[ip2 * L + j];    // (-2,0)
-    acc += R[i * L + jm2];    // (0,2)
-    acc += R[i * L + jp2];    // (0,-2)
-    acc += R[im1 * L + jm1];  // (1,1)
-    acc += R[im1 * L + jp1];  // (1,-1)
-    acc += R[ip1 * L + jm1];  // (-1,1)
-    acc += R[ip1 * L + jp1];  // (-1,-1)
-    return (acc / 13.0) > 0.0 ? 1 : 0;
-  } else {
-    return (acc / 5.0) > 0.0 ? 1 : 0;
-  }
-}
-
-// Value slots of the act reduction.
-enum {
-  V_PCT = 0, V_Q = 1, V_QC = 5, V_QD = 9,                 // -> slot t-1
-  V_SUMP = 13, V_SUMP_C, V_SUMP_D, V_SUMR,                // -> slot t
-  V_SWCD, V_SWDC, V_WPP, V_WRR, V_REWC, V_REWD, V_RATIO,  // -> slot t
-  V_NCOOP1,                                               // -> slot t+1
-  V_ACT_N
-};
-static_assert(V_ACT_N <= 32, "act reduction holds 32 values");
-
-__device__ __forceinline__ int act_stat_index(int k, int* slot_delta) {
-  if (k == V_PCT) { *slot_delta = -1; return SPGG_ST_SUM_PCT; }
-  if (k < V_QC) { *slot_delta = -1; return SPGG_ST_SUMQ + (k - V_Q); }
-  if (k < V_QD) { *slot_delta = -1; return SPGG_ST_SUMQ_C + (k - V_QC); }
-  if (k < V_SUMP) { *slot_delta = -1; return SPGG_ST_SUMQ_D + (k - V_QD); }
-  *slot_delta = 0;
-  switch (k) {
-    case V_SUMP: return SPGG_ST_SUMP;
-    case V_SUMP_C: return SPGG_ST_SUMP_C;
-    case V_SUMP_D: return SPGG_ST_SUMP_D;
-    case V_SUMR: return SPGG_ST_SUMR;
-    case V_SWCD: return SPGG_ST_SW_CD;
-    case V_SWDC: return SPGG_ST_SW_DC;
-    case V_WPP: return SPGG_ST_SUM_WPP;
-    case V_WRR: return SPGG_ST_SUM_WRR;
-    case V_REWC: return SPGG_ST_SUM_REW_C;
-    case V_REWD: return SPGG_ST_SUM_REW_D;
-    case V_RATIO: return SPGG_ST_SUM_RATIO_C;
-    case V_NCOOP1: *slot_delta = 1; return SPGG_ST_NCOOP;
-    default: return -1;
-  }
-}
-
-// ---------------------------------------------------------------------------
-template <bool M2, bool ACTION_STATE, int RNG>
-__global__ __launch_bounds__(kBlock) void spgg_act_kernel(KArgs a, int t, int finalize_only) {
-  __shared__ double lds[kWaves * 32];
-  const int rep = blockIdx.y;
+  // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
+  // dispatch), so give them consecutive tiles of one replica (shared halos).
+  const int total = a.n_rep * a.tiles_per_rep;
+  const int per_xcd = (total + 7) / 8;
+  const int logical = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (logical >= total) return;
+  const int rep = logical / a.tiles_per_rep;
+  const int tile = logical - rep * a.tiles_per_rep;
   const int st = a.stop_iter[rep];
-  if (st != 0 && st < t) return;  // replica absorbed before t: nothing to do
-  const spgg_rep_params p = a.params[rep];
+  if (st != 0 && st < t) return;  // absorbed before t
+
   const int L = a.L, n = a.n;
-  const size_t rb = (size_t)rep * n;
+  const int tyi = tile / a.tiles_x, txi = tile - (tile / a.tiles_x) * a.tiles_x;
+  const int y0 = tyi * a.TH, x0 = txi * a.TW;
+  const int th = min(a.TH, L - y0), tw = min(a.TW, L - x0);
+  const LdsLayout ly = lds_layout(tw, th, HS, HR, HA);
+  double* tab = reinterpret_cast<double*>(smem);
+  double* red = tab + 12;
+  double* sR = reinterpret_cast<double*>(smem + ly.off_R);
+  double* sRn = reinterpret_cast<double*>(smem + ly.off_Rn);
+  double* sRew = reinterpret_cast<double*>(smem + ly.off_Rew);
+  uint8_t* sS = smem + ly.off_S;
+  uint8_t* sA = smem + ly.off_A;
+
+  const spgg_rep_params& pg = a.params[rep];
+  const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
   double* srow = a.stats + (size_t)rep * a.slots * SPGG_NSTAT;
-  const bool has_pending = t > 1;
   bool stop_now = false;
-  if (!finalize_only) {
+  if (!fin_only) {
     const double nc = srow[(size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
     stop_now = (nc == 0.0) || (nc == (double)n);  // spgg.py:405
-    if (stop_now && blockIdx.x == 0 && threadIdx.x == 0) a.stop_iter[rep] = t;
+    if (stop_now && tile == 0 && threadIdx.x == 0) a.stop_iter[rep] = t;
   }
-  double lam_den = 0.0;
-  if (has_pending) lam_den = srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + p.lambda_eps;
+  const bool acting = !fin_only && !stop_now;
+  const bool pending = t > 1;
+  const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
+  const size_t rb = (size_t)rep * n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  double v[32];
+  // ---- phase 0: owned-agent registers + LDS staging ----------------------
+  int gidx[APT];
+  double q[APT][4];
+  double md_own[APT];
+  float atd_own[APT];
+  const int n_own = th * tw;
 #pragma unroll
-  for (int k = 0; k < 32; ++k) v[k] = 0.0;
-
-  const int beg = blockIdx.x * a.chunk;
-  const int end = min(beg + a.chunk, n);
-  for (int idx = beg + (int)threadIdx.x; idx < end; idx += kBlock) {
-    const size_t g = rb + idx;
-    const int i = idx / L, j = idx - (idx / L) * L;
-    const int s_t = a.S_cur[g];
-    double2* qp = reinterpret_cast<double2*>(a.Q + g * 4);
-    const double2 q01 = qp[0], q23 = qp[1];
-    double q[4] = {q01.x, q01.y, q23.x, q23.y};
-
-    if (has_pending) {  // NI of iteration t-1, spgg.py:489-509 + 511-513, 561-583
-      const int ax = a.aux[g];
-      const int so = ax & 1, ps = (ax >> 1) & 1, dp = (ax >> 2) & 1;
-      const double md = a.ni_md[g], atd = a.ni_atd[g];
-      const double lam = (p.kappa * md) / lam_den;
-      const double nu = lam * (dp ? 1.0 : -1.0);
-      const int e = so * 2 + s_t;  // S_t is the action of iteration t-1
-      const double qn = q_get(q, e) + nu;
-      q_set(q, e, qn);
-      a.Q[g * 4 + e] = qn;
-      const double anu = fabs(nu);
-      v[V_PCT] += anu / ((atd + anu) + 1e-8) * 100.0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[V_Q + k] += q[k];
-        if (ps == 0) v[V_QC + k] += q[k]; else v[V_QD + k] += q[k];
+  for (int u = 0; u < APT; ++u) {
+    const int k = tid + u * kBlock;
+    gidx[u] = -1;
+    md_own[u] = 0.0;
+    atd_own[u] = 0.f;
+    q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
+    if (k < n_own) {
+      const int r = k / tw, c = k - (k / tw) * tw;
+      gidx[u] = (y0 + r) * L + (x0 + c);
+      const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + gidx[u]) * 4);
+      const double2 q01 = qp[0], q23 = qp[1];
+      q[u][0] = q01.x; q[u][1] = q01.y; q[u][2] = q23.x; q[u][3] = q23.y;
+      if (pending) {
+        md_own[u] = a.md_in[rb + gidx[u]];
+        atd_own[u] = a.atd[rb + gidx[u]];
       }
     }
-    if (finalize_only) continue;
-
-    // iteration-start record, spgg.py:373-394
-    const double P = payoff(a.S_cur + rb, i, j, L, p);
-    const double r_t = a.R_cur[g];
-    v[V_SUMP] += P;
-    if (s_t == 0) v[V_SUMP_C] += P; else v[V_SUMP_D] += P;
-    v[V_SUMR] += r_t;
-    if (stop_now) continue;
-
-    // old state, spgg.py:409
-    int so;
-    if constexpr (ACTION_STATE) so = (s_t == 0) ? 1 : 0;
-    else so = rep_state<M2>(a.R_cur + rb, i, j, L);
-
-    // eps-greedy, algorithms.py:105-109
-    int explore, rb_bit;
-    if constexpr (RNG == SPGG_RNG_PHILOX) {
-      const uint4 w = philox4x32_10(make_uint4((uint32_t)idx, (uint32_t)t, (uint32_t)rep, 0x53504747u),
-                                    (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
-      explore = mt_double(w.x, w.y) < eps_t ? 1 : 0;
-      rb_bit = (int)(w.z & 1u);
-    } else {
-      explore = a.explore[g];
-      rb_bit = a.rbit[g];
-    }
-    const double qs0 = so ? q[2] : q[0], qs1 = so ? q[3] : q[1];
-    const int greedy = (qs0 >= qs1) ? 0 : 1;  // argmax, ties -> 0
-    const int act = explore ? rb_bit : greedy;
-
-    // reputation, spgg.py:319-323
-    double rn = r_t + (act == 0 ? p.rep_gain_c : p.neg_delta_r_d);
-    rn = fmin(fmax(rn, p.r_min), p.r_max);
-    a.R_nxt[g] = rn;
-    a.S_nxt[g] = (uint8_t)act;
-
-    // reward, spgg.py:424-427
-    const double rr = (act == 0) ? 0.5 : 0.0;
-    const double wpp = p.w_p * P, wrr = p.w_rep * rr;
-    const double rew = wpp + wrr;
-    a.reward[g] = rew;
-    a.aux[g] = (uint8_t)(so | (s_t << 1));
-
-    v[V_SWCD] += (s_t == 0 && act == 1) ? 1.0 : 0.0;
-    v[V_SWDC] += (s_t == 1 && act == 0) ? 1.0 : 0.0;
-    v[V_NCOOP1] += (act == 0) ? 1.0 : 0.0;
-    v[V_WPP] += wpp;
-    v[V_WRR] += wrr;
-    if (act == 0) {
-      v[V_REWC] += rew;
-      v[V_RATIO] += (fabs(wrr) / (fabs(rew) + 1e-9)) * 100.0;
-    } else {
-      v[V_REWD] += rew;
+  }
+  if (tid < 12) tab[tid] = tid < 6 ? pg.pay_c[tid] : pg.pay_d[tid - 6];
+  {
+    const uint8_t* Sg = a.S_in + rb;
+    for (int row = wave; row < ly.sh; row += kWaves) {
+      const int gi = wrap(y0 - HS + row, L);
+      for (int col = lane; col < ly.sw; col += 64) sS[row * ly.sw + col] = Sg[gi * L + wrap(x0 - HS + col, L)];
     }
   }
-
-  const double tot = block_reduce<32>(v, lds);
-  if (threadIdx.x < V_ACT_N) {
-    int dslot;
-    const int k = act_stat_index(threadIdx.x, &dslot);
-    const bool used = (dslot < 0) ? has_pending : !finalize_only;
-    if (used && tot != 0.0) atomicAdd(&srow[(size_t)(t + dslot) * SPGG_NSTAT + k], tot);
-  }
-}
-
-// ---------------------------------------------------------------------------
-template <bool M2, bool ACTION_STATE>
-__global__ __launch_bounds__(kBlock) void spgg_learn_kernel(KArgs a, int t) {
-  __shared__ double lds[kWaves * 8 + kWaves];
-  const int rep = blockIdx.y;
-  const int st = a.stop_iter[rep];
-  if (st != 0 && st <= t) return;
-  const spgg_rep_params p = a.params[rep];
-  const int L = a.L, n = a.n;
-  const size_t rb = (size_t)rep * n;
-  const uint8_t* S1 = a.S_nxt + rb;
-  const double* rw = a.reward + rb;
-  double* srow = a.stats + (size_t)rep * a.slots * SPGG_NSTAT;
-
-  double v[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = 0.0;
-  double bmax = 0.0;
-
-  const int beg = blockIdx.x * a.chunk;
-  const int end = min(beg + a.chunk, n);
-  for (int idx = beg + (int)threadIdx.x; idx < end; idx += kBlock) {
-    const size_t g = rb + idx;
-    const int i = idx / L, j = idx - (idx / L) * L;
-    const int act = S1[idx];
-    const int ax = a.aux[g];
-    const int so = ax & 1;
-    int sn;  // new state, spgg.py:423
-    if constexpr (ACTION_STATE) sn = (act == 0) ? 1 : 0;
-    else sn = rep_state<M2>(a.R_nxt + rb, i, j, L);
-    const double rew = rw[idx];
-
-    // Q-learning TD update, algorithms.py:121-131
-    double2* qp = reinterpret_cast<double2*>(a.Q + g * 4);
-    const double2 q01 = qp[0], q23 = qp[1];
-    double q[4] = {q01.x, q01.y, q23.x, q23.y};
-    const int e = so * 2 + act;
-    const double qc = q_get(q, e);
-    const double m = sn ? fmax(q[2], q[3]) : fmax(q[0], q[1]);
-    const double td = (rew + p.gamma * m) - qc;
-    const double q1 = qc + p.alpha * td;
-    q_set(q, e, q1);
-    a.Q[g * 4 + e] = q1;
-    // diagnostic TD on the updated table, spgg.py:446-473
-    const double m2 = sn ? fmax(q[2], q[3]) : fmax(q[0], q[1]);
-    const double td2 = (rew + p.diag_gamma * m2) - q1;
-    const double atd = fabs(p.diag_alpha * td2);
-
-    // neighbor influence, spgg.py:477-494: d_k = roll(rew, o_k) - rew,
-    // roll(X,(dx,dy))[i,j] = X[i-dx, j-dy]; first argmax wins ties.
-    const int im1 = wrap(i - 1, L), ip1 = wrap(i + 1, L);
-    const int jm1 = wrap(j - 1, L), jp1 = wrap(j + 1, L);
-    constexpr int K = M2 ? 12 : 4;
-    int nb[K];
-    nb[0] = im1 * L + j;  // (1,0)
-    nb[1] = ip1 * L + j;  // (-1,0)
-    nb[2] = i * L + jm1;  // (0,1)
-    nb[3] = i * L + jp1;  // (0,-1)
-    if constexpr (M2) {
-      const int im2 = wrap(i - 2, L), ip2 = wrap(i + 2, L);
-      const int jm2 = wrap(j - 2, L), jp2 = wrap(j + 2, L);
-      nb[4] = im2 * L + j;    // (2,0)
-      nb[5] = ip2 * L + j;    // (-2,0)
-      nb[6] = i * L + jm2;    // (0,2)
-      nb[7] = i * L + jp2;    // (0,-2)
-      nb[8] = im1 * L + jm1;  // (1,1)
-      nb[9] = im1 * L + jp1;  // (1,-1)
-      nb[10] = ip1 * L + jm1; // (-1,1)
-      nb[11] = ip1 * L + jp1; // (-1,-1)
+  if (!AS && !fin_only) {
+    const double* Rg = a.R_in + rb;
+    for (int row = wave; row < ly.rh; row += kWaves) {
+      const int gi = wrap(y0 - HR + row, L);
+      for (int col = lane; col < ly.rw; col += 64) sR[row * ly.rw + col] = Rg[gi * L + wrap(x0 - HR + col, L)];
     }
-    double md = rw[nb[0]] - rew;
-    int ks = 0;
-#pragma unroll
-    for (int k = 1; k < K; ++k) {
-      const double d = rw[nb[k]] - rew;
-      if (d > md) { md = d; ks = k; }
-    }
-    int ksel = nb[0];
-#pragma unroll
-    for (int k = 1; k < K; ++k) ksel = (ks == k) ? nb[k] : ksel;
-    const int dp = (S1[ksel] == act) ? 1 : 0;
-    const double mdp = md > 0.0 ? md : 0.0;
-    a.ni_md[g] = mdp;
-    a.ni_atd[g] = atd;
-    a.aux[g] = (uint8_t)(ax | (dp << 2));
-    bmax = fmax(bmax, mdp);
-
-    // group composition on S_{t+1}, spgg.py:585-592
-    const int nd = act + S1[im1 * L + j] + S1[ip1 * L + j] + S1[i * L + jm1] + S1[i * L + jp1];
-#pragma unroll
-    for (int d = 0; d < 6; ++d) v[d] += (nd == d) ? 1.0 : 0.0;
-    if (md > 0.0) {  // spgg.py:520-523
-      v[6] += 1.0;
-      if (ks >= 4) v[7] += 1.0;
-    }
-  }
-
-  const double tot = block_reduce<8>(v, lds);
-  double* slot = srow + (size_t)t * SPGG_NSTAT;
-  if (threadIdx.x < 8 && tot != 0.0) {
-    const int k = threadIdx.x < 6 ? SPGG_ST_GC0 + threadIdx.x
-                                  : (threadIdx.x == 6 ? SPGG_ST_NMD_POS : SPGG_ST_NMD_POS2);
-    atomicAdd(&slot[k], tot);
   }
   __syncthreads();
-  const double bm = block_reduce_max(bmax, lds + kWaves * 8);
-  if (threadIdx.x == 0 && bm > 0.0) {
-    // non-negative doubles order like their bit patterns (spgg.py:488)
-    atomicMax(reinterpret_cast<unsigned long long*>(&slot[SPGG_ST_GMAX]),
-              (unsigned long long)__double_as_longlong(bm));
+
+  // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
+  {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = 0.0;
+    if (pending) {
+#pragma unroll
+      for (int u = 0; u < APT; ++u) {
+        if (gidx[u] < 0) continue;
+        const int k = tid + u * kBlock;
+        const int r = k / tw, c = k - (k / tw) * tw;
+        const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
+        const double nu = apply_pending(q[u], b, md_own[u], kappa, lam_den);
+        const double anu = fabs(nu);
+        v[F_PCT] += anu / (((double)atd_own[u] + anu) + 1e-8) * 100.0;  // spgg.py:512
+        const bool prev_c = ((b >> 3) & 1) == 0;                          // prev_S of t-1
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {                                     // spgg.py:562-583
+          v[F_Q + e] += q[u][e];
+          if (prev_c) v[F_QC + e] += q[u][e]; else v[F_QD + e] += q[u][e];
+        }
+      }
+    }
+    wave_partials<16>(v, red, 0);
+  }
+  if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
+#pragma unroll
+    for (int u = 0; u < APT; ++u) {
+      if (gidx[u] < 0) continue;
+      double2* qo = reinterpret_cast<double2*>(a.Q_out + (rb + gidx[u]) * 4);
+      qo[0] = make_double2(q[u][0], q[u][1]);
+      qo[1] = make_double2(q[u][2], q[u][3]);
+    }
+  }
+
+  // ---- phase 1b: iteration start + action select for owned agents --------
+  int own_bits[APT];  // a | so<<1 | s_t<<3
+  {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = 0.0;
+#pragma unroll
+    for (int u = 0; u < APT; ++u) {
+      own_bits[u] = 0;
+      if (fin_only || gidx[u] < 0) continue;
+      const int k = tid + u * kBlock;
+      const int r = k / tw, c = k - (k / tw) * tw;
+      const int cs = (r + HS) * ly.sw + (c + HS);
+      const int s_t = sS[cs] & 1;
+      const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
+      const double r_t = AS ? a.R_in[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
+      v[A_SUMP] += P;                                       // spgg.py:388-390
+      if (s_t == 0) v[A_SUMP_C] += P; else v[A_SUMP_D] += P;
+      v[A_SUMR] += r_t;                                     // spgg.py:394
+      if (!acting) continue;
+      int so;                                               // spgg.py:409
+      if constexpr (AS) so = s_t == 0 ? 1 : 0;
+      else so = rep_state_lds<M2>(sR, (r + HR) * ly.rw + (c + HR), ly.rw);
+      int ex, rbt;                                          // algorithms.py:105-109
+      if constexpr (RNG == SPGG_RNG_PHILOX) {
+        philox_draw(gidx[u], t, rep, pg.seed, eps_t, &ex, &rbt);
+      } else {
+        ex = a.explore[rb + gidx[u]];
+        rbt = a.rbit[rb + gidx[u]];
+      }
+      const double qs0 = so ? q[u][2] : q[u][0], qs1 = so ? q[u][3] : q[u][1];
+      const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);    // argmax ties -> 0
+      double rn = r_t + (act == 0 ? pg.rep_gain_c : pg.neg_delta_r_d);  // spgg.py:321-323
+      rn = fmin(fmax(rn, pg.r_min), pg.r_max);
+      const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
+      const double wpp = w_p * P, wrr = w_rep * rr;
+      const double rew = wpp + wrr;
+      const int ca = (r + HA) * ly.aw + (c + HA);
+      sA[ca] = (uint8_t)act;
+      sRn[ca] = rn;
+      sRew[ca] = rew;
+      a.R_out[rb + gidx[u]] = rn;
+      own_bits[u] = act | (so << 1) | (s_t << 3);
+      v[A_SWCD] += (s_t == 0 && act == 1) ? 1.0 : 0.0;      // spgg.py:419-420
+      v[A_SWDC] += (s_t == 1 && act == 0) ? 1.0 : 0.0;
+      v[A_NCOOP1] += act == 0 ? 1.0 : 0.0;
+      v[A_WPP] += wpp;                                      // spgg.py:425-426
+      v[A_WRR] += wrr;
+      if (act == 0) {                                       // spgg.py:529-545
+        v[A_REWC] += rew;
+        v[A_RATIO] += (fabs(wrr) / (fabs(rew) + 1e-9)) * 100.0;
+      } else {
+        v[A_REWD] += rew;
+      }
+    }
+    wave_partials<16>(v, red, 16);
+  }
+
+  // ---- phase 1c: recompute the ring of neighbours (distance <= M) --------
+  if (acting) {
+    const int band = HA * ly.aw;
+    const int ring = ly.aw * ly.ah - n_own;
+    for (int k = tid; k < ring; k += kBlock) {
+      int ay, ax;
+      if (k < band) {
+        ay = k / ly.aw;
+        ax = k - ay * ly.aw;
+      } else if (k < 2 * band) {
+        const int k2 = k - band;
+        ay = HA + th + k2 / ly.aw;
+        ax = k2 - (k2 / ly.aw) * ly.aw;
+      } else {
+        const int k3 = k - 2 * band;
+        ay = HA + k3 / (2 * HA);
+        const int cc = k3 - (k3 / (2 * HA)) * (2 * HA);
+        ax = cc < HA ? cc : tw + cc;
+      }
+      const int g = wrap(y0 - HA + ay, L) * L + wrap(x0 - HA + ax, L);
+      const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
+      const uint8_t b = sS[cs];
+      const int s_t = b & 1;
+      const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + g) * 4);
+      const double2 q01 = qp[0], q23 = qp[1];
+      double qq[4] = {q01.x, q01.y, q23.x, q23.y};
+      if (pending) apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den);
+      const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
+      int so;
+      double r_t;
+      if constexpr (AS) {
+        so = s_t == 0 ? 1 : 0;
+        r_t = 0.0;  // R of ring agents is not needed in action-state mode
+      } else {
+        const int cr = (ay + (HR - HA)) * ly.rw + (ax + (HR - HA));
+        so = rep_state_lds<M2>(sR, cr, ly.rw);
+        r_t = sR[cr];
+      }
+      int ex, rbt;
+      if constexpr (RNG == SPGG_RNG_PHILOX) {
+        philox_draw(g, t, rep, pg.seed, eps_t, &ex, &rbt);
+      } else {
+        ex = a.explore[rb + g];
+        rbt = a.rbit[rb + g];
+      }
+      const double qs0 = so ? qq[2] : qq[0], qs1 = so ? qq[3] : qq[1];
+      const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);
+      double rn = r_t + (act == 0 ? pg.rep_gain_c : pg.neg_delta_r_d);
+      rn = fmin(fmax(rn, pg.r_min), pg.r_max);
+      const double rew = w_p * P + w_rep * (act == 0 ? 0.5 : 0.0);
+      const int ca = ay * ly.aw + ax;
+      sA[ca] = (uint8_t)act;
+      sRn[ca] = rn;
+      sRew[ca] = rew;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: learn for owned agents -----------------------------------
+  double bmax = 0.0;
+  {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.0;
+    if (acting) {
+      const double alpha = pg.alpha, gamma = pg.gamma, dalpha = pg.diag_alpha, dgamma = pg.diag_gamma;
+#pragma unroll
+      for (int u = 0; u < APT; ++u) {
+        if (gidx[u] < 0) continue;
+        const int k = tid + u * kBlock;
+        const int r = k / tw, c = k - (k / tw) * tw;
+        const int ca = (r + HA) * ly.aw + (c + HA);
+        const int act = own_bits[u] & 1, so = (own_bits[u] >> 1) & 1;
+        const double rew = sRew[ca];
+        int sn;                                               // spgg.py:423
+        if constexpr (AS) sn = act == 0 ? 1 : 0;
+        else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
+        // Q-learning TD, algorithms.py:121-131
+        const int e = so * 2 + act;
+        const double qc = q_get(q[u], e);
+        const double m = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
+        const double td = (rew + gamma * m) - qc;
+        const double q1 = qc + alpha * td;
+        q_set(q[u], e, q1);
+        double2* qo = reinterpret_cast<double2*>(a.Q_out + (rb + gidx[u]) * 4);
+        qo[0] = make_double2(q[u][0], q[u][1]);
+        qo[1] = make_double2(q[u][2], q[u][3]);
+        // diagnostic TD on the updated table, spgg.py:446-473
+        const double m2 = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
+        const double td2 = (rew + dgamma * m2) - q1;
+        a.atd[rb + gidx[u]] = (float)fabs(dalpha * td2);
+        // neighbour influence, spgg.py:477-494: first argmax wins ties
+        const int w = ly.aw;
+        constexpr int KN = M2 ? 12 : 4;
+        const int nb[12] = {ca - w, ca + w, ca - 1, ca + 1,
+                            ca - 2 * w, ca + 2 * w, ca - 2, ca + 2,
+                            ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
+        double md = sRew[nb[0]] - rew;
+        int ks = 0;
+#pragma unroll
+        for (int kk = 1; kk < KN; ++kk) {
+          const double d = sRew[nb[kk]] - rew;
+          if (d > md) {
+            md = d;
+            ks = kk;
+          }
+        }
+        int sel = nb[0];
+#pragma unroll
+        for (int kk = 1; kk < KN; ++kk) sel = ks == kk ? nb[kk] : sel;
+        const int dp = sA[sel] == act ? 1 : 0;
+        const double mdp = md > 0.0 ? md : 0.0;
+        a.md_out[rb + gidx[u]] = mdp;
+        bmax = fmax(bmax, mdp);
+        a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2));
+        // group composition on S_{t+1}, spgg.py:585-592
+        const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) v[L_GC + d] += nd == d ? 1.0 : 0.0;
+        if (md > 0.0) {                                       // spgg.py:520-523
+          v[L_NMD] += 1.0;
+          if (ks >= 4) v[L_NMD2] += 1.0;
+        }
+      }
+    }
+    wave_partials<8>(v, red, 32);
+  }
+  __syncthreads();
+
+  // ---- workgroup totals -> per-iteration history record ------------------
+  if (tid < 40) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tot += red[w * 64 + tid];
+    int slot = -1, k = -1;
+    if (tid < F_N) {
+      if (pending) {
+        slot = t - 1;
+        k = tid == F_PCT ? SPGG_ST_SUM_PCT
+          : tid < F_QC   ? SPGG_ST_SUMQ + (tid - F_Q)
+          : tid < F_QD   ? SPGG_ST_SUMQ_C + (tid - F_QC)
+                         : SPGG_ST_SUMQ_D + (tid - F_QD);
+      }
+    } else if (tid >= 16 && tid < 16 + A_N && !fin_only) {
+      const int j = tid - 16;
+      if (acting || j <= A_SUMR) {
+        slot = j == A_NCOOP1 ? t + 1 : t;
+        k = j == A_SUMP ? SPGG_ST_SUMP : j == A_SUMP_C ? SPGG_ST_SUMP_C : j == A_SUMP_D ? SPGG_ST_SUMP_D
+          : j == A_SUMR ? SPGG_ST_SUMR : j == A_SWCD ? SPGG_ST_SW_CD : j == A_SWDC ? SPGG_ST_SW_DC
+          : j == A_WPP ? SPGG_ST_SUM_WPP : j == A_WRR ? SPGG_ST_SUM_WRR : j == A_REWC ? SPGG_ST_SUM_REW_C
+          : j == A_REWD ? SPGG_ST_SUM_REW_D : j == A_RATIO ? SPGG_ST_SUM_RATIO_C : SPGG_ST_NCOOP;
+      }
+    } else if (tid >= 32 && tid < 32 + L_N && acting) {
+      const int j = tid - 32;
+      slot = t;
+      k = j < 6 ? SPGG_ST_GC0 + j : (j == L_NMD ? SPGG_ST_NMD_POS : SPGG_ST_NMD_POS2);
+    }
+    if (slot >= 0 && tot != 0.0) atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], tot);
+  }
+  if (acting) {
+    __syncthreads();
+    const double bm = block_reduce_max(bmax, red);
+    if (tid == 0 && bm > 0.0) {
+      // non-negative doubles order like their bit patterns (spgg.py:488)
+      atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
+                (unsigned long long)__double_as_longlong(bm));
+    }
   }
 }
 
@@ -571,12 +586,24 @@ __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
 // P of every agent from S_t (epilogue: SPGG.P / run()'s mean(P), spgg.py:378, 637).
 __global__ __launch_bounds__(kBlock) void spgg_payoff_kernel(const uint8_t* S, const spgg_rep_params* params,
                                                              double* out, int L, int n) {
+  __shared__ double tab[12];
   const int rep = blockIdx.y;
+  if (threadIdx.x < 12)
+    tab[threadIdx.x] = threadIdx.x < 6 ? params[rep].pay_c[threadIdx.x] : params[rep].pay_d[threadIdx.x - 6];
+  __syncthreads();
   const int idx = blockIdx.x * kBlock + threadIdx.x;
   if (idx >= n) return;
-  const spgg_rep_params p = params[rep];
+  const uint8_t* s = S + (size_t)rep * n;
   const int i = idx / L, j = idx - (idx / L) * L;
-  out[(size_t)rep * n + idx] = payoff(S + (size_t)rep * n, i, j, L, p);
+  const int im1 = wrap(i - 1, L), ip1 = wrap(i + 1, L), im2 = wrap(i - 2, L), ip2 = wrap(i + 2, L);
+  const int jm1 = wrap(j - 1, L), jp1 = wrap(j + 1, L), jm2 = wrap(j - 2, L), jp2 = wrap(j + 2, L);
+#define CO(r, c) ((s[(r) * L + (c)] & 1) ? 0 : 1)
+  Cells13 c;
+  c.c00 = CO(i, j); c.cm0 = CO(im1, j); c.cp0 = CO(ip1, j); c.c0m = CO(i, jm1); c.c0p = CO(i, jp1);
+  c.cmm = CO(im1, jm1); c.cmp = CO(im1, jp1); c.cpm = CO(ip1, jm1); c.cpp = CO(ip1, jp1);
+  c.cM0 = CO(im2, j); c.cP0 = CO(ip2, j); c.c0M = CO(i, jm2); c.c0P = CO(i, jp2);
+#undef CO
+  out[(size_t)rep * n + idx] = payoff13(c, tab, params[rep].norm_min, params[rep].norm_den);
 }
 
 }  // namespace
@@ -590,8 +617,8 @@ struct spgg_ctx {
   bool params_set = false;
   spgg_rep_params* d_params = nullptr;
   int n = 0;
-  int chunk = kBlock;
-  int blocks_x = 1;
+  int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4;
+  size_t lds_bytes = 0;
   std::string err;
 };
 
@@ -607,18 +634,37 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
   return fail(c, SPGG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-KArgs make_args(const spgg_ctx* c, int t) {
-  KArgs a{};
+// Tile shape: <= 1024 agents, rows >= 16 wide when L allows; minimise padded
+// lanes + halo recompute per agent (L=200 -> 40x25, L=1000 -> 40x25).
+void choose_tile(int L, int* TW, int* TH) {
+  int best_w = std::min(L, 32), best_h = std::min(L, 32);
+  double best = 1e300;
+  for (int w = std::min(L, 16); w <= std::min(L, 64); ++w) {
+    for (int h = 1; h <= std::min(L, 64); ++h) {
+      if (w * h > 1024) break;
+      const int tx = (L + w - 1) / w, ty = (L + h - 1) / h;
+      const double slots = (double)tx * ty * ((w * h + kBlock - 1) / kBlock) * kBlock;
+      const double halo = (double)tx * ty * ((w + 4) * (h + 4) - w * h);
+      const double cost = (slots + 2.0 * halo) / ((double)L * L);
+      if (cost < best - 1e-12 || (cost <= best + 1e-12 && w > best_w)) {  // ties: wider rows
+        best = cost;
+        best_w = w;
+        best_h = h;
+      }
+    }
+  }
+  *TW = best_w;
+  *TH = best_h;
+}
+
+TileArgs make_args(const spgg_ctx* c, int t) {
+  TileArgs a{};
   const int cur = (t - 1) & 1, nxt = t & 1;
-  a.S_cur = c->buf.S[cur];
-  a.S_nxt = c->buf.S[nxt];
-  a.R_cur = c->buf.R[cur];
-  a.R_nxt = c->buf.R[nxt];
-  a.Q = c->buf.Q;
-  a.reward = c->buf.reward;
-  a.aux = c->buf.aux;
-  a.ni_md = c->buf.ni_md;
-  a.ni_atd = c->buf.ni_atd;
+  a.S_in = c->buf.S[cur];   a.S_out = c->buf.S[nxt];
+  a.R_in = c->buf.R[cur];   a.R_out = c->buf.R[nxt];
+  a.Q_in = c->buf.Q[cur];   a.Q_out = c->buf.Q[nxt];
+  a.md_in = c->buf.md[cur]; a.md_out = c->buf.md[nxt];
+  a.atd = c->buf.atd;
   a.explore = c->buf.explore;
   a.rbit = c->buf.rbit;
   a.eps = c->buf.eps;
@@ -627,44 +673,41 @@ KArgs make_args(const spgg_ctx* c, int t) {
   a.params = c->d_params;
   a.L = c->cfg.L;
   a.n = c->n;
-  a.chunk = c->chunk;
+  a.TW = c->TW;
+  a.TH = c->TH;
+  a.tiles_x = c->tiles_x;
+  a.tiles_per_rep = c->tiles_per_rep;
+  a.n_rep = c->cfg.n_rep;
   a.slots = c->cfg.iterations + 2;
   return a;
 }
 
 template <bool M2, bool AS, int RNG>
-void launch_act(const KArgs& a, dim3 grid, int t, int fin, hipStream_t s) {
-  hipLaunchKernelGGL((spgg_act_kernel<M2, AS, RNG>), grid, dim3(kBlock), 0, s, a, t, fin);
+void launch_step_t(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
+  const int total = c->cfg.n_rep * c->tiles_per_rep;
+  const dim3 grid(((total + 7) / 8) * 8);
+  if (c->apt <= 2)
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RNG, 2>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
+  else
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RNG, 4>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
 }
 
 template <bool M2, bool AS>
-void launch_act_rng(const KArgs& a, dim3 grid, int t, int fin, int rng, hipStream_t s) {
-  if (rng == SPGG_RNG_PHILOX) launch_act<M2, AS, SPGG_RNG_PHILOX>(a, grid, t, fin, s);
-  else launch_act<M2, AS, SPGG_RNG_MT19937>(a, grid, t, fin, s);  // INJECT reads the same bytes
+void launch_step_rng(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (c->cfg.rng_mode == SPGG_RNG_PHILOX) launch_step_t<M2, AS, SPGG_RNG_PHILOX>(c, a, t, fin, s);
+  else launch_step_t<M2, AS, SPGG_RNG_MT19937>(c, a, t, fin, s);  // INJECT reads the same bytes
 }
 
-void launch_act_any(const spgg_ctx* c, const KArgs& a, dim3 grid, int t, int fin, hipStream_t s) {
-  const bool m2 = c->cfg.second_order != 0;
-  const bool as = c->cfg.state_mode == SPGG_STATE_ACTION;
-  const int rng = c->cfg.rng_mode;
-  if (m2) {
-    if (as) launch_act_rng<true, true>(a, grid, t, fin, rng, s);
-    else launch_act_rng<true, false>(a, grid, t, fin, rng, s);
-  } else {
-    if (as) launch_act_rng<false, true>(a, grid, t, fin, rng, s);
-    else launch_act_rng<false, false>(a, grid, t, fin, rng, s);
-  }
-}
-
-void launch_learn_any(const spgg_ctx* c, const KArgs& a, dim3 grid, int t, hipStream_t s) {
+void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
+  const TileArgs a = make_args(c, t);
   const bool m2 = c->cfg.second_order != 0;
   const bool as = c->cfg.state_mode == SPGG_STATE_ACTION;
   if (m2) {
-    if (as) hipLaunchKernelGGL((spgg_learn_kernel<true, true>), grid, dim3(kBlock), 0, s, a, t);
-    else hipLaunchKernelGGL((spgg_learn_kernel<true, false>), grid, dim3(kBlock), 0, s, a, t);
+    if (as) launch_step_rng<true, true>(c, a, t, fin, s);
+    else launch_step_rng<true, false>(c, a, t, fin, s);
   } else {
-    if (as) hipLaunchKernelGGL((spgg_learn_kernel<false, true>), grid, dim3(kBlock), 0, s, a, t);
-    else hipLaunchKernelGGL((spgg_learn_kernel<false, false>), grid, dim3(kBlock), 0, s, a, t);
+    if (as) launch_step_rng<false, true>(c, a, t, fin, s);
+    else launch_step_rng<false, false>(c, a, t, fin, s);
   }
 }
 
@@ -689,23 +732,26 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     return SPGG_E_ARG;
   if (cfg->state_mode != SPGG_STATE_REPUTATION && cfg->state_mode != SPGG_STATE_ACTION) return SPGG_E_ARG;
   if (cfg->rng_mode < SPGG_RNG_INJECT || cfg->rng_mode > SPGG_RNG_PHILOX) return SPGG_E_ARG;
-  if (cfg->n_rep > 65535) return SPGG_E_ARG;
+  if ((long long)cfg->n_rep * cfg->L * cfg->L > (1LL << 31) - 1) return SPGG_E_ARG;
   spgg_ctx* c = new (std::nothrow) spgg_ctx();
   if (!c) return SPGG_E_ARG;
   c->cfg = *cfg;
   c->n = cfg->L * cfg->L;
-  // Agents per workgroup: grow while the batch still fills >= 2048 workgroups.
-  int apt = 1;
-  while (apt < 8) {
-    const long long per = (long long)kBlock * apt * 2;
-    const long long blocks = (long long)cfg->n_rep * ((c->n + per - 1) / per);
-    if (blocks < 2048) break;
-    apt *= 2;
+  choose_tile(cfg->L, &c->TW, &c->TH);
+  c->tiles_x = (cfg->L + c->TW - 1) / c->TW;
+  c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
+  c->apt = (c->TW * c->TH + kBlock - 1) / kBlock <= 2 ? 2 : 4;
+  const int HA = cfg->second_order ? 2 : 1;
+  c->lds_bytes = (size_t)lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA).bytes;
+  if (c->lds_bytes > 160 * 1024) {
+    delete c;
+    return SPGG_E_ARG;
   }
-  c->chunk = kBlock * apt;
-  c->blocks_x = (c->n + c->chunk - 1) / c->chunk;
   int rc = hip_check(c, hipSetDevice(cfg->device), "hipSetDevice");
-  if (rc) { delete c; return rc; }
+  if (rc) {
+    delete c;
+    return rc;
+  }
   *out = c;
   return SPGG_OK;
 }
@@ -727,15 +773,17 @@ int spgg_set_params(spgg_ctx* c, const spgg_rep_params* params) {
 
 int spgg_bind(spgg_ctx* c, const spgg_buffers* b) {
   if (!c || !b) return fail(c, SPGG_E_ARG, "null argument");
-  if (!b->S[0] || !b->S[1] || !b->R[0] || !b->R[1] || !b->Q || !b->reward || !b->aux || !b->ni_md ||
-      !b->ni_atd || !b->eps || !b->stats || !b->stop_iter)
+  for (int i = 0; i < 2; ++i)
+    if (!b->S[i] || !b->R[i] || !b->Q[i] || !b->md[i])
+      return fail(c, SPGG_E_ARG, "spgg_bind: a ping-pong buffer is null");
+  if (!b->atd || !b->eps || !b->stats || !b->stop_iter)
     return fail(c, SPGG_E_ARG, "spgg_bind: a required buffer is null");
   if (c->cfg.rng_mode != SPGG_RNG_PHILOX && (!b->explore || !b->rbit))
     return fail(c, SPGG_E_ARG, "spgg_bind: explore/rbit buffers required for INJECT/MT19937");
   if (c->cfg.rng_mode == SPGG_RNG_MT19937 && !b->mt_state)
     return fail(c, SPGG_E_ARG, "spgg_bind: mt_state required for MT19937");
-  if ((reinterpret_cast<uintptr_t>(b->Q) & 15) != 0)
-    return fail(c, SPGG_E_ARG, "spgg_bind: Q must be 16-byte aligned");
+  if (((reinterpret_cast<uintptr_t>(b->Q[0]) | reinterpret_cast<uintptr_t>(b->Q[1])) & 15) != 0)
+    return fail(c, SPGG_E_ARG, "spgg_bind: Q buffers must be 16-byte aligned");
   c->buf = *b;
   c->bound = true;
   return SPGG_OK;
@@ -749,12 +797,9 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
   if (c->cfg.rng_mode == SPGG_RNG_INJECT && n_steps > 1)
     return fail(c, SPGG_E_ARG, "spgg_step: INJECT mode steps one iteration per call");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid(c->blocks_x, c->cfg.n_rep);
   for (int t = t0; t < t0 + n_steps; ++t) {
-    const KArgs a = make_args(c, t);
     if (c->cfg.rng_mode == SPGG_RNG_MT19937) launch_draw(c, t, s);
-    launch_act_any(c, a, grid, t, 0, s);
-    launch_learn_any(c, a, grid, t, s);
+    launch_step(c, t, 0, s);
   }
   return hip_check(c, hipGetLastError(), "spgg_step launch");
 }
@@ -763,9 +808,7 @@ int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {
   if (!c) return SPGG_E_ARG;
   if (!c->bound || !c->params_set) return fail(c, SPGG_E_STATE, "spgg_flush before bind/set_params");
   if (t_last < 1 || t_last > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_flush: bad t_last");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid(c->blocks_x, c->cfg.n_rep);
-  launch_act_any(c, make_args(c, t_last + 1), grid, t_last + 1, 1, s);
+  launch_step(c, t_last + 1, 1, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_flush launch");
 }
 
@@ -786,6 +829,13 @@ int spgg_payoff(spgg_ctx* c, int32_t t, double* out, void* stream) {
   hipLaunchKernelGGL(spgg_payoff_kernel, grid, dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                      c->buf.S[(t - 1) & 1], c->d_params, out, c->cfg.L, c->n);
   return hip_check(c, hipGetLastError(), "spgg_payoff launch");
+}
+
+int spgg_tile_shape(const spgg_ctx* c, int32_t* tw, int32_t* th) {
+  if (!c || !tw || !th) return SPGG_E_ARG;
+  *tw = c->TW;
+  *th = c->TH;
+  return SPGG_OK;
 }
 
 int spgg_destroy(spgg_ctx* c) {

@@ -17,8 +17,8 @@ Random streams:
 """
 from __future__ import annotations
 
+import ctypes
 import dataclasses
-import math
 from typing import Callable, Optional, Sequence
 
 import numpy as np
@@ -73,6 +73,11 @@ class ReplicaParams:
         p.r_min = float(self.R_min)
         p.r_max = float(self.R_max)
         p.seed = int(self.seed or 0) & 0xFFFFFFFFFFFFFFFF
+        rc = r * c
+        for N in range(6):                               # spgg.py:256-257, N cooperators
+            tk = rc * N / 5
+            p.pay_c[N] = float(tk - self.cost)
+            p.pay_d[N] = float(tk)
         return p
 
 
@@ -148,11 +153,10 @@ class BatchEngine:
         self.S = torch.zeros((2, R, n), dtype=u8, device=d)
         self.S[0].copy_(torch.from_numpy(S0))
         self.Rep = torch.zeros((2, R, n), dtype=f64, device=d)
-        self.Q = torch.from_numpy(Q0).to(d).contiguous()
-        self.reward = torch.zeros((R, n), dtype=f64, device=d)
-        self.aux = torch.zeros((R, n), dtype=u8, device=d)
-        self.ni_md = torch.zeros((R, n), dtype=f64, device=d)
-        self.ni_atd = torch.zeros((R, n), dtype=f64, device=d)
+        self.Qb = torch.zeros((2, R, n, 4), dtype=f64, device=d)
+        self.Qb[0].copy_(torch.from_numpy(Q0))
+        self.md = torch.zeros((2, R, n), dtype=f64, device=d)
+        self.atd = torch.zeros((R, n), dtype=torch.float32, device=d)
         self.explore = torch.zeros((R, n), dtype=u8, device=d)
         self.rbit = torch.zeros((R, n), dtype=u8, device=d)
         mt = np.zeros((R, 625), dtype=np.uint32)
@@ -182,22 +186,24 @@ class BatchEngine:
         cfg = C.Config(device=self.dev.index, n_rep=self.R, L=self.L, second_order=int(self.M2),
                        state_mode=C.STATE_ACTION if self.state_rep == "action" else C.STATE_REPUTATION,
                        rng_mode=C.RNG_MODES[self.rng], iterations=self.T, reserved=0)
-        ctx = __import__("ctypes").c_void_p()
-        C.check(self.lib.spgg_create(__import__("ctypes").byref(ctx), cfg), None, "spgg_create")
+        ctx = ctypes.c_void_p()
+        C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
         self.ctx = ctx
         arr = (C.RepParams * self.R)(*[p.to_c() for p in self.reps])
         C.check(self.lib.spgg_set_params(self.ctx, arr), self.ctx, "spgg_set_params")
         b = C.Buffers()
-        b.S[0], b.S[1] = self.S[0].data_ptr(), self.S[1].data_ptr()
-        b.R[0], b.R[1] = self.Rep[0].data_ptr(), self.Rep[1].data_ptr()
-        b.Q = self.Q.data_ptr()
-        b.reward, b.aux = self.reward.data_ptr(), self.aux.data_ptr()
-        b.ni_md, b.ni_atd = self.ni_md.data_ptr(), self.ni_atd.data_ptr()
+        for i in range(2):
+            b.S[i], b.R[i] = self.S[i].data_ptr(), self.Rep[i].data_ptr()
+            b.Q[i], b.md[i] = self.Qb[i].data_ptr(), self.md[i].data_ptr()
+        b.atd = self.atd.data_ptr()
         b.explore, b.rbit = self.explore.data_ptr(), self.rbit.data_ptr()
         b.mt_state = self.mt_state.data_ptr()
         b.eps, b.stats, b.stop_iter = self.eps.data_ptr(), self.stats.data_ptr(), self.stop_iter.data_ptr()
         self._bufs = b
         C.check(self.lib.spgg_bind(self.ctx, b), self.ctx, "spgg_bind")
+        tw, th = ctypes.c_int32(), ctypes.c_int32()
+        C.check(self.lib.spgg_tile_shape(self.ctx, ctypes.byref(tw), ctypes.byref(th)), self.ctx, "tile")
+        self.tile = (tw.value, th.value)
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -286,7 +292,7 @@ class BatchEngine:
         strategies after iteration t-1 for the PNG snapshot (spgg.py:553-559)."""
         stop = self.stop_iter.cpu().numpy()
         cur = (t - 1) & 1
-        S = self.S[cur].cpu().numpy()
+        S = self.S[cur].cpu().numpy() & 1
         Rn = self.Rep[cur].cpu().numpy() if snap else None
         for k in range(self.R):
             if stop[k] != 0:
@@ -307,11 +313,14 @@ class BatchEngine:
         """(Q (L,L,2,2), R (L,L), S (L,L) int64) of replica k after the run."""
         last = self.last_iteration(k)
         s = int(self.stopped[k])
-        cur = (last - 1) & 1 if s else last & 1   # S_{last} if absorbed, else S_{last+1}
+        if s:   # absorbed at s: S_s, R_s untouched since; Q finalized by launch s
+            cur, qb = (s - 1) & 1, s & 1
+        else:   # S_{last+1}, R_{last+1}; Q finalized by the flush launch last+1
+            cur, qb = last & 1, (last + 1) & 1
         L = self.L
-        Q = self.Q[k].cpu().numpy().reshape(L, L, 2, 2)
+        Q = self.Qb[qb, k].cpu().numpy().reshape(L, L, 2, 2)
         R = self.Rep[cur, k].cpu().numpy().reshape(L, L)
-        S = self.S[cur, k].cpu().numpy().reshape(L, L).astype(np.int64)
+        S = (self.S[cur, k].cpu().numpy() & 1).reshape(L, L).astype(np.int64)
         return Q, R, S
 
     def payoff_at(self, t):

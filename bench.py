@@ -185,7 +185,7 @@ def main():
                        "rng": args.rng, "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "act+learn (one iteration)",
+                         "kernel": "spgg_step_kernel (one launch per iteration)" if args.rng == "philox" else "spgg_mt_draw_kernel + spgg_step_kernel",
                          "device_ms_per_step": per_step_dev_s * 1e3},
         }
         if world == 1 and not args.no_cpu_baseline:

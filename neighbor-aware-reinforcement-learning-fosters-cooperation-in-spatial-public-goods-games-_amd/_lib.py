@@ -68,7 +68,7 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("SPGG_LIB") or LIB_PATH  # SPGG_LIB: tuning builds only
         if not os.path.exists(p):
             raise SpggError(f"{p} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
         lib = ctypes.CDLL(p)

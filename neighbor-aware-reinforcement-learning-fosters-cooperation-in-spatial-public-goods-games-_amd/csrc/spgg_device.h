@@ -98,13 +98,27 @@ __device__ __forceinline__ double mt_double(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
 }
 
-// eps-greedy draw of agent `idx` at iteration t (Philox mode): explore flag + random action.
-__device__ __forceinline__ void philox_draw(int idx, int t, int rep, uint64_t seed, double eps,
-                                            int* explore, int* rbit) {
-  const uint4 w = philox4x32_10(make_uint4((uint32_t)idx, (uint32_t)t, (uint32_t)rep, 0x53504747u),
-                                (uint32_t)seed, (uint32_t)(seed >> 32));
+// Philox2x32-10 (Salmon et al. 2011; Crush-resistant at 10 rounds): 64 bits
+// per (counter, key) at half the cost of the 4x32 variant.
+__device__ __forceinline__ uint2 philox2x32_10(uint2 c, uint32_t k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) k += 0x9E3779B9u;
+    const uint32_t lo = 0xD256D193u * c.x, hi = __umulhi(0xD256D193u, c.x);
+    c = make_uint2(hi ^ k ^ c.y, lo);
+  }
+  return c;
+}
+
+// eps-greedy draw of agent `idx` at iteration t (Philox mode): counter
+// (agent, iteration), key = replica seed mixed with the replica index.
+// u takes 53 bits (w.x>>5, w.y>>6) exactly as numpy's random_sample; the
+// random action is the low bit of w.y, which u does not use.
+__device__ __forceinline__ void philox_draw(int idx, int t, uint32_t key, double eps, int* explore,
+                                            int* rbit) {
+  const uint2 w = philox2x32_10(make_uint2((uint32_t)idx, (uint32_t)t), key);
   *explore = mt_double(w.x, w.y) < eps ? 1 : 0;  // algorithms.py:105
-  *rbit = (int)(w.z & 1u);                        // algorithms.py:108
+  *rbit = (int)(w.y & 1u);                        // algorithms.py:108
 }
 
 // q[4] accessors with a run-time index, kept in registers (no scratch).

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -38,6 +40,12 @@
 #include "spgg_device.h"
 
 using namespace spgg;
+
+// Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
+//   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute
+#ifndef SPGG_ABLATE
+#define SPGG_ABLATE 0
+#endif
 
 namespace {
 
@@ -61,16 +69,6 @@ struct TileArgs {
   const spgg_rep_params* params;
   int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
 };
-
-// Value slots of the workgroup reductions.
-enum { F_PCT = 0, F_Q = 1, F_QC = 5, F_QD = 9, F_N = 13 };  // -> slot t-1
-enum {
-  A_SUMP = 0, A_SUMP_C, A_SUMP_D, A_SUMR,                   // -> slot t
-  A_SWCD, A_SWDC, A_WPP, A_WRR, A_REWC, A_REWD, A_RATIO,    // -> slot t
-  A_NCOOP1,                                                 // -> slot t+1
-  A_N
-};
-enum { L_GC = 0, L_NMD = 6, L_NMD2 = 7, L_N = 8 };           // -> slot t
 
 struct LdsLayout {
   int sw, sh, rw, rh, aw, ah;
@@ -147,6 +145,54 @@ __device__ __forceinline__ void wave_partials(double (&v)[K], double* red, int b
   if ((lane & (per - 1)) == 0) red[wave * 64 + base + lane / per] = v[0];
 }
 
+// Periodic index for x in [-L, 2L) (every halo offset here is <= 4 < L
+// once L >= 8); tiny lattices take the general loop.
+__device__ __forceinline__ int wrap1(int x, int L, bool tiny) {
+  if (tiny) return wrap(x, L);
+  x += x < 0 ? L : 0;
+  x -= x >= L ? L : 0;
+  return x;
+}
+
+// Copy an h x w window of a periodic L x L plane (origin y0, x0; may wrap)
+// into LDS.  Every global load of the thread is issued before the first LDS
+// store, so the whole window costs one memory round trip (J >= h*w/kBlock).
+template <int J, typename T>
+__device__ __forceinline__ void stage_region(T* dst, const T* src, int h, int w, int y0, int x0, int L,
+                                             bool tiny) {
+  const int total = h * w;
+  const int tid = threadIdx.x;
+  const int dr = kBlock / w, dc = kBlock - (kBlock / w) * w;
+  int r = tid / w, c = tid - (tid / w) * w;
+  T buf[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if (tid + j * kBlock < total) buf[j] = src[wrap1(y0 + r, L, tiny) * L + wrap1(x0 + c, L, tiny)];
+    r += dr;
+    c += dc;
+    if (c >= w) {
+      c -= w;
+      ++r;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    if (tid + j * kBlock < total) dst[tid + j * kBlock] = buf[j];
+}
+
+// 1/x to full f64 precision for DIAGNOSTIC quotients only (history values,
+// tolerance 1e-5): hardware estimate + two Newton steps, no IEEE division.
+__device__ __forceinline__ double rcp_diag(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+  return r;
+}
+
+// Packed 8-bit per-thread counters (a thread owns <= 4 agents).
+enum { C_SWCD = 0, C_SWDC = 8, C_NCOOP1 = 16, C_NMD = 24 };   // cnt0
+enum { C_NMD2 = 0, C_GC0 = 8 };                                // cnt1: GC0..2 at 8,16,24; cnt2: GC3..5
+
 template <bool M2, bool AS, int RNG, int APT>
 __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
@@ -166,6 +212,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   if (st != 0 && st < t) return;  // absorbed before t
 
   const int L = a.L, n = a.n;
+  const bool tiny = L < 8;
   const int tyi = tile / a.tiles_x, txi = tile - (tile / a.tiles_x) * a.tiles_x;
   const int y0 = tyi * a.TH, x0 = txi * a.TW;
   const int th = min(a.TH, L - y0), tw = min(a.TW, L - x0);
@@ -192,51 +239,53 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
   const size_t rb = (size_t)rep * n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
+  // Philox key: 64-bit seed folded with the replica index (distinct streams per replica)
+  const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^ (uint32_t)rep * 0xC2B2AE35u;
 
   // ---- phase 0: owned-agent registers + LDS staging ----------------------
-  int gidx[APT];
+  // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
+  int gidx[APT], rc[APT];
   double q[APT][4];
   double md_own[APT];
   float atd_own[APT];
   const int n_own = th * tw;
+  {
+    const int dr = kBlock / tw, dc = kBlock - (kBlock / tw) * tw;
+    int r = tid / tw, c = tid - (tid / tw) * tw;
 #pragma unroll
-  for (int u = 0; u < APT; ++u) {
-    const int k = tid + u * kBlock;
-    gidx[u] = -1;
-    md_own[u] = 0.0;
-    atd_own[u] = 0.f;
-    q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
-    if (k < n_own) {
-      const int r = k / tw, c = k - (k / tw) * tw;
-      gidx[u] = (y0 + r) * L + (x0 + c);
-      const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + gidx[u]) * 4);
-      const double2 q01 = qp[0], q23 = qp[1];
-      q[u][0] = q01.x; q[u][1] = q01.y; q[u][2] = q23.x; q[u][3] = q23.y;
-      if (pending) {
-        md_own[u] = a.md_in[rb + gidx[u]];
-        atd_own[u] = a.atd[rb + gidx[u]];
+    for (int u = 0; u < APT; ++u) {
+      const int k = tid + u * kBlock;
+      gidx[u] = -1;
+      rc[u] = (r << 16) | c;
+      md_own[u] = 0.0;
+      atd_own[u] = 0.f;
+      q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
+      if (k < n_own) {
+        gidx[u] = (y0 + r) * L + (x0 + c);
+        const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + gidx[u]) * 4);
+        const double2 q01 = qp[0], q23 = qp[1];
+        q[u][0] = q01.x; q[u][1] = q01.y; q[u][2] = q23.x; q[u][3] = q23.y;
+        if (pending) {
+          md_own[u] = a.md_in[rb + gidx[u]];
+          atd_own[u] = a.atd[rb + gidx[u]];
+        }
+      }
+      r += dr;
+      c += dc;
+      if (c >= tw) {
+        c -= tw;
+        ++r;
       }
     }
   }
   if (tid < 12) tab[tid] = tid < 6 ? pg.pay_c[tid] : pg.pay_d[tid - 6];
-  {
-    const uint8_t* Sg = a.S_in + rb;
-    for (int row = wave; row < ly.sh; row += kWaves) {
-      const int gi = wrap(y0 - HS + row, L);
-      for (int col = lane; col < ly.sw; col += 64) sS[row * ly.sw + col] = Sg[gi * L + wrap(x0 - HS + col, L)];
-    }
-  }
-  if (!AS && !fin_only) {
-    const double* Rg = a.R_in + rb;
-    for (int row = wave; row < ly.rh; row += kWaves) {
-      const int gi = wrap(y0 - HR + row, L);
-      for (int col = lane; col < ly.rw; col += 64) sR[row * ly.rw + col] = Rg[gi * L + wrap(x0 - HR + col, L)];
-    }
-  }
+  stage_region<(M2 ? 8 : 7)>(sS, a.S_in + rb, ly.sh, ly.sw, y0 - HS, x0 - HS, L, tiny);
+  if (!AS && !fin_only) stage_region<(M2 ? 8 : 6)>(sR, a.R_in + rb, ly.rh, ly.rw, y0 - HR, x0 - HR, L, tiny);
   __syncthreads();
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
+  // value slots: 0 pct, 1-4 sum Q, 5-8 sum Q over prev C  (-> slot t-1)
   {
     double v[16];
 #pragma unroll
@@ -245,17 +294,16 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
         if (gidx[u] < 0) continue;
-        const int k = tid + u * kBlock;
-        const int r = k / tw, c = k - (k / tw) * tw;
+        const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
         const double nu = apply_pending(q[u], b, md_own[u], kappa, lam_den);
         const double anu = fabs(nu);
-        v[F_PCT] += anu / (((double)atd_own[u] + anu) + 1e-8) * 100.0;  // spgg.py:512
-        const bool prev_c = ((b >> 3) & 1) == 0;                          // prev_S of t-1
+        v[0] += (anu * rcp_diag(((double)atd_own[u] + anu) + 1e-8)) * 100.0;  // spgg.py:512
+        const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                        // prev_S of t-1 == C
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {                                     // spgg.py:562-583
-          v[F_Q + e] += q[u][e];
-          if (prev_c) v[F_QC + e] += q[u][e]; else v[F_QD + e] += q[u][e];
+        for (int e = 0; e < 4; ++e) {                                          // spgg.py:562-583
+          v[1 + e] += q[u][e];
+          v[5 + e] += q[u][e] * cm;
         }
       }
     }
@@ -272,65 +320,67 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   }
 
   // ---- phase 1b: iteration start + action select for owned agents --------
+  // f64 value slots (-> slot t): 0 sumP, 1 sumP over C, 2 sumR, 3 sum w_P*P,
+  // 4 sum w_rep*rr, 5 sum reward, 6 sum reward over C, 7 sum ratio over C
+  double va[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) va[k] = 0.0;
+  unsigned cnt0 = 0, cnt1 = 0, cnt2 = 0;
   int own_bits[APT];  // a | so<<1 | s_t<<3
-  {
-    double v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = 0.0;
-#pragma unroll
-    for (int u = 0; u < APT; ++u) {
-      own_bits[u] = 0;
-      if (fin_only || gidx[u] < 0) continue;
-      const int k = tid + u * kBlock;
-      const int r = k / tw, c = k - (k / tw) * tw;
-      const int cs = (r + HS) * ly.sw + (c + HS);
-      const int s_t = sS[cs] & 1;
-      const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
-      const double r_t = AS ? a.R_in[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
-      v[A_SUMP] += P;                                       // spgg.py:388-390
-      if (s_t == 0) v[A_SUMP_C] += P; else v[A_SUMP_D] += P;
-      v[A_SUMR] += r_t;                                     // spgg.py:394
-      if (!acting) continue;
-      int so;                                               // spgg.py:409
-      if constexpr (AS) so = s_t == 0 ? 1 : 0;
-      else so = rep_state_lds<M2>(sR, (r + HR) * ly.rw + (c + HR), ly.rw);
-      int ex, rbt;                                          // algorithms.py:105-109
-      if constexpr (RNG == SPGG_RNG_PHILOX) {
-        philox_draw(gidx[u], t, rep, pg.seed, eps_t, &ex, &rbt);
-      } else {
-        ex = a.explore[rb + gidx[u]];
-        rbt = a.rbit[rb + gidx[u]];
-      }
-      const double qs0 = so ? q[u][2] : q[u][0], qs1 = so ? q[u][3] : q[u][1];
-      const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);    // argmax ties -> 0
-      double rn = r_t + (act == 0 ? pg.rep_gain_c : pg.neg_delta_r_d);  // spgg.py:321-323
-      rn = fmin(fmax(rn, pg.r_min), pg.r_max);
-      const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
-      const double wpp = w_p * P, wrr = w_rep * rr;
-      const double rew = wpp + wrr;
-      const int ca = (r + HA) * ly.aw + (c + HA);
-      sA[ca] = (uint8_t)act;
-      sRn[ca] = rn;
-      sRew[ca] = rew;
-      a.R_out[rb + gidx[u]] = rn;
-      own_bits[u] = act | (so << 1) | (s_t << 3);
-      v[A_SWCD] += (s_t == 0 && act == 1) ? 1.0 : 0.0;      // spgg.py:419-420
-      v[A_SWDC] += (s_t == 1 && act == 0) ? 1.0 : 0.0;
-      v[A_NCOOP1] += act == 0 ? 1.0 : 0.0;
-      v[A_WPP] += wpp;                                      // spgg.py:425-426
-      v[A_WRR] += wrr;
-      if (act == 0) {                                       // spgg.py:529-545
-        v[A_REWC] += rew;
-        v[A_RATIO] += (fabs(wrr) / (fabs(rew) + 1e-9)) * 100.0;
-      } else {
-        v[A_REWD] += rew;
-      }
+  for (int u = 0; u < APT; ++u) {
+    own_bits[u] = 0;
+    if (fin_only || gidx[u] < 0) continue;
+    const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+    const int cs = (r + HS) * ly.sw + (c + HS);
+    const int s_t = sS[cs] & 1;
+    const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
+    const double r_t = AS ? a.R_in[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
+    const double cmask = s_t ? 0.0 : 1.0;
+    va[0] += P;                                           // spgg.py:388-390
+    va[1] += P * cmask;
+    va[2] += r_t;                                         // spgg.py:394
+    if (!acting) continue;
+    int so;                                               // spgg.py:409
+    if constexpr (AS) so = s_t == 0 ? 1 : 0;
+    else so = rep_state_lds<M2>(sR, (r + HR) * ly.rw + (c + HR), ly.rw);
+    int ex, rbt;                                          // algorithms.py:105-109
+    if constexpr (RNG == SPGG_RNG_PHILOX) {
+#if SPGG_ABLATE & 1
+      ex = ((gidx[u] * 2654435761u + t) >> 7) % 50 == 0; rbt = (gidx[u] ^ t) & 1;
+#else
+      philox_draw(gidx[u], t, pkey, eps_t, &ex, &rbt);
+#endif
+    } else {
+      ex = a.explore[rb + gidx[u]];
+      rbt = a.rbit[rb + gidx[u]];
     }
-    wave_partials<16>(v, red, 16);
+    const double qs0 = so ? q[u][2] : q[u][0], qs1 = so ? q[u][3] : q[u][1];
+    const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);    // argmax ties -> 0
+    double rn = r_t + (act == 0 ? pg.rep_gain_c : pg.neg_delta_r_d);  // spgg.py:321-323
+    rn = fmin(fmax(rn, pg.r_min), pg.r_max);
+    const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
+    const double wpp = w_p * P, wrr = w_rep * rr;
+    const double rew = wpp + wrr;
+    const int ca = (r + HA) * ly.aw + (c + HA);
+    sA[ca] = (uint8_t)act;
+    sRn[ca] = rn;
+    sRew[ca] = rew;
+    a.R_out[rb + gidx[u]] = rn;
+    own_bits[u] = act | (so << 1) | (s_t << 3);
+    cnt0 += ((s_t == 0 && act == 1) ? 1u : 0u) << C_SWCD;  // spgg.py:419-420
+    cnt0 += ((s_t == 1 && act == 0) ? 1u : 0u) << C_SWDC;
+    cnt0 += (act == 0 ? 1u : 0u) << C_NCOOP1;
+    va[3] += wpp;                                         // spgg.py:425-426
+    va[4] += wrr;
+    va[5] += rew;                                         // spgg.py:529-545
+    const double am = act ? 0.0 : 1.0;
+    va[6] += rew * am;
+    va[7] += ((fabs(wrr) * rcp_diag(fabs(rew) + 1e-9)) * 100.0) * am;
   }
 
   // ---- phase 1c: recompute the ring of neighbours (distance <= M) --------
-  if (acting) {
+  if (acting && !(SPGG_ABLATE & 4)) {
     const int band = HA * ly.aw;
     const int ring = ly.aw * ly.ah - n_own;
     for (int k = tid; k < ring; k += kBlock) {
@@ -348,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         const int cc = k3 - (k3 / (2 * HA)) * (2 * HA);
         ax = cc < HA ? cc : tw + cc;
       }
-      const int g = wrap(y0 - HA + ay, L) * L + wrap(x0 - HA + ax, L);
+      const int g = wrap1(y0 - HA + ay, L, tiny) * L + wrap1(x0 - HA + ax, L, tiny);
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
       const uint8_t b = sS[cs];
       const int s_t = b & 1;
@@ -369,7 +419,11 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       }
       int ex, rbt;
       if constexpr (RNG == SPGG_RNG_PHILOX) {
-        philox_draw(g, t, rep, pg.seed, eps_t, &ex, &rbt);
+#if SPGG_ABLATE & 1
+        ex = ((g * 2654435761u + t) >> 7) % 50 == 0; rbt = (g ^ t) & 1;
+#else
+        philox_draw(g, t, pkey, eps_t, &ex, &rbt);
+#endif
       } else {
         ex = a.explore[rb + g];
         rbt = a.rbit[rb + g];
@@ -389,104 +443,123 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
 
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;
-  {
-    double v[8];
+  if (acting) {
+    const double alpha = pg.alpha, gamma = pg.gamma, dalpha = pg.diag_alpha, dgamma = pg.diag_gamma;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = 0.0;
-    if (acting) {
-      const double alpha = pg.alpha, gamma = pg.gamma, dalpha = pg.diag_alpha, dgamma = pg.diag_gamma;
+    for (int u = 0; u < APT; ++u) {
+      if (gidx[u] < 0) continue;
+      const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+      const int ca = (r + HA) * ly.aw + (c + HA);
+      const int act = own_bits[u] & 1, so = (own_bits[u] >> 1) & 1;
+      const double rew = sRew[ca];
+      int sn;                                               // spgg.py:423
+      if constexpr (AS) sn = act == 0 ? 1 : 0;
+      else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
+      // Q-learning TD, algorithms.py:121-131
+      const int e = so * 2 + act;
+      const double qc = q_get(q[u], e);
+      const double m = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
+      const double td = (rew + gamma * m) - qc;
+      const double q1 = qc + alpha * td;
+      q_set(q[u], e, q1);
+      double2* qo = reinterpret_cast<double2*>(a.Q_out + (rb + gidx[u]) * 4);
+      qo[0] = make_double2(q[u][0], q[u][1]);
+      qo[1] = make_double2(q[u][2], q[u][3]);
+      // diagnostic TD on the updated table, spgg.py:446-473
+      const double m2 = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
+      const double td2 = (rew + dgamma * m2) - q1;
+      a.atd[rb + gidx[u]] = (float)fabs(dalpha * td2);
+      // neighbour influence, spgg.py:477-494: first argmax wins ties
+      const int w = ly.aw;
+      constexpr int KN = M2 ? 12 : 4;
+      const int nb[12] = {ca - w, ca + w, ca - 1, ca + 1,
+                          ca - 2 * w, ca + 2 * w, ca - 2, ca + 2,
+                          ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
+      double md = sRew[nb[0]] - rew;
+      int sel = nb[0], ks = 0;
 #pragma unroll
-      for (int u = 0; u < APT; ++u) {
-        if (gidx[u] < 0) continue;
-        const int k = tid + u * kBlock;
-        const int r = k / tw, c = k - (k / tw) * tw;
-        const int ca = (r + HA) * ly.aw + (c + HA);
-        const int act = own_bits[u] & 1, so = (own_bits[u] >> 1) & 1;
-        const double rew = sRew[ca];
-        int sn;                                               // spgg.py:423
-        if constexpr (AS) sn = act == 0 ? 1 : 0;
-        else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-        // Q-learning TD, algorithms.py:121-131
-        const int e = so * 2 + act;
-        const double qc = q_get(q[u], e);
-        const double m = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
-        const double td = (rew + gamma * m) - qc;
-        const double q1 = qc + alpha * td;
-        q_set(q[u], e, q1);
-        double2* qo = reinterpret_cast<double2*>(a.Q_out + (rb + gidx[u]) * 4);
-        qo[0] = make_double2(q[u][0], q[u][1]);
-        qo[1] = make_double2(q[u][2], q[u][3]);
-        // diagnostic TD on the updated table, spgg.py:446-473
-        const double m2 = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
-        const double td2 = (rew + dgamma * m2) - q1;
-        a.atd[rb + gidx[u]] = (float)fabs(dalpha * td2);
-        // neighbour influence, spgg.py:477-494: first argmax wins ties
-        const int w = ly.aw;
-        constexpr int KN = M2 ? 12 : 4;
-        const int nb[12] = {ca - w, ca + w, ca - 1, ca + 1,
-                            ca - 2 * w, ca + 2 * w, ca - 2, ca + 2,
-                            ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
-        double md = sRew[nb[0]] - rew;
-        int ks = 0;
-#pragma unroll
-        for (int kk = 1; kk < KN; ++kk) {
-          const double d = sRew[nb[kk]] - rew;
-          if (d > md) {
-            md = d;
-            ks = kk;
-          }
-        }
-        int sel = nb[0];
-#pragma unroll
-        for (int kk = 1; kk < KN; ++kk) sel = ks == kk ? nb[kk] : sel;
-        const int dp = sA[sel] == act ? 1 : 0;
-        const double mdp = md > 0.0 ? md : 0.0;
-        a.md_out[rb + gidx[u]] = mdp;
-        bmax = fmax(bmax, mdp);
-        a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2));
-        // group composition on S_{t+1}, spgg.py:585-592
-        const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
-#pragma unroll
-        for (int d = 0; d < 6; ++d) v[L_GC + d] += nd == d ? 1.0 : 0.0;
-        if (md > 0.0) {                                       // spgg.py:520-523
-          v[L_NMD] += 1.0;
-          if (ks >= 4) v[L_NMD2] += 1.0;
+      for (int kk = 1; kk < KN; ++kk) {
+        const double d = sRew[nb[kk]] - rew;
+        if (d > md) {
+          md = d;
+          sel = nb[kk];
+          ks = kk;
         }
       }
+      const int dp = sA[sel] == act ? 1 : 0;
+      const double mdp = md > 0.0 ? md : 0.0;
+      a.md_out[rb + gidx[u]] = mdp;
+      bmax = fmax(bmax, mdp);
+      a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2));
+      // group composition on S_{t+1}, spgg.py:585-592
+      const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
+      if (nd < 3) cnt1 += 1u << (C_GC0 + 8 * nd);
+      else cnt2 += 1u << (8 * (nd - 3));
+      if (md > 0.0) {                                       // spgg.py:520-523
+        cnt0 += 1u << C_NMD;
+        if (ks >= 4) cnt1 += 1u << C_NMD2;
+      }
     }
-    wave_partials<8>(v, red, 32);
+  }
+  {  // slot layout in red[wave*64 + 16 ..]: va[0..7], then 11 counts
+    double v[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = va[k];
+    v[8] = (double)((cnt0 >> C_SWCD) & 0xff);
+    v[9] = (double)((cnt0 >> C_SWDC) & 0xff);
+    v[10] = (double)((cnt0 >> C_NCOOP1) & 0xff);
+    v[11] = (double)((cnt0 >> C_NMD) & 0xff);
+    v[12] = (double)((cnt1 >> C_NMD2) & 0xff);
+    v[13] = (double)((cnt1 >> 8) & 0xff);
+    v[14] = (double)((cnt1 >> 16) & 0xff);
+    v[15] = (double)((cnt1 >> 24) & 0xff);
+    v[16] = (double)(cnt2 & 0xff);
+    v[17] = (double)((cnt2 >> 8) & 0xff);
+    v[18] = (double)((cnt2 >> 16) & 0xff);
+#pragma unroll
+    for (int k = 19; k < 32; ++k) v[k] = 0.0;
+    wave_partials<32>(v, red, 16);
   }
   __syncthreads();
 
   // ---- workgroup totals -> per-iteration history record ------------------
-  if (tid < 40) {
-    double tot = 0.0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) tot += red[w * 64 + tid];
-    int slot = -1, k = -1;
-    if (tid < F_N) {
+  if (tid < 64) {
+    double tot[2] = {0.0, 0.0};  // this slot and (for derived values) its "C" partner
+    int slot = -1, k = -1, src = -1, src_c = -1;
+    // Finalize group (slot t-1): sums over prev-D are total - prev-C.
+    if (tid < 13) {
       if (pending) {
         slot = t - 1;
-        k = tid == F_PCT ? SPGG_ST_SUM_PCT
-          : tid < F_QC   ? SPGG_ST_SUMQ + (tid - F_Q)
-          : tid < F_QD   ? SPGG_ST_SUMQ_C + (tid - F_QC)
-                         : SPGG_ST_SUMQ_D + (tid - F_QD);
+        if (tid == 0) { k = SPGG_ST_SUM_PCT; src = 0; }
+        else if (tid < 5) { k = SPGG_ST_SUMQ + tid - 1; src = tid; }
+        else if (tid < 9) { k = SPGG_ST_SUMQ_C + tid - 5; src = tid; }
+        else { k = SPGG_ST_SUMQ_D + tid - 9; src = tid - 8; src_c = tid - 4; }
       }
-    } else if (tid >= 16 && tid < 16 + A_N && !fin_only) {
+    } else if (tid >= 16 && tid < 16 + 22 && !fin_only) {
       const int j = tid - 16;
-      if (acting || j <= A_SUMR) {
-        slot = j == A_NCOOP1 ? t + 1 : t;
-        k = j == A_SUMP ? SPGG_ST_SUMP : j == A_SUMP_C ? SPGG_ST_SUMP_C : j == A_SUMP_D ? SPGG_ST_SUMP_D
-          : j == A_SUMR ? SPGG_ST_SUMR : j == A_SWCD ? SPGG_ST_SW_CD : j == A_SWDC ? SPGG_ST_SW_DC
-          : j == A_WPP ? SPGG_ST_SUM_WPP : j == A_WRR ? SPGG_ST_SUM_WRR : j == A_REWC ? SPGG_ST_SUM_REW_C
-          : j == A_REWD ? SPGG_ST_SUM_REW_D : j == A_RATIO ? SPGG_ST_SUM_RATIO_C : SPGG_ST_NCOOP;
-      }
-    } else if (tid >= 32 && tid < 32 + L_N && acting) {
-      const int j = tid - 32;
-      slot = t;
-      k = j < 6 ? SPGG_ST_GC0 + j : (j == L_NMD ? SPGG_ST_NMD_POS : SPGG_ST_NMD_POS2);
+      static constexpr int kmap[22] = {
+          SPGG_ST_SUMP, SPGG_ST_SUMP_C, SPGG_ST_SUMR, SPGG_ST_SUM_WPP, SPGG_ST_SUM_WRR,
+          -1 /* reward total: only feeds REW_D */, SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C,
+          SPGG_ST_SW_CD, SPGG_ST_SW_DC, SPGG_ST_NCOOP, SPGG_ST_NMD_POS, SPGG_ST_NMD_POS2,
+          SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2, SPGG_ST_GC0 + 3, SPGG_ST_GC0 + 4,
+          SPGG_ST_GC0 + 5, SPGG_ST_SUMP_D, SPGG_ST_SUM_REW_D, -1};
+      k = kmap[j];
+      src = 16 + j;
+      if (j == 19) { src = 16 + 0; src_c = 16 + 1; }   // sumP over D = sumP - sumP over C
+      if (j == 20) { src = 16 + 5; src_c = 16 + 6; }   // reward over D = total - over C
+      const bool start_val = (j <= 2 || j == 19);      // recorded on the absorbing iteration too
+      if (k >= 0 && (acting || start_val)) slot = (j == 10) ? t + 1 : t;
     }
-    if (slot >= 0 && tot != 0.0) atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], tot);
+    if (slot >= 0) {
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        tot[0] += red[w * 64 + src];
+        if (src_c >= 0) tot[1] += red[w * 64 + src_c];
+      }
+      const double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
+      if (val != 0.0 && (!(SPGG_ABLATE & 2) || k == SPGG_ST_NCOOP))
+        atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);
+    }
   }
   if (acting) {
     __syncthreads();
@@ -738,12 +811,22 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->cfg = *cfg;
   c->n = cfg->L * cfg->L;
   choose_tile(cfg->L, &c->TW, &c->TH);
+  if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
+    int w = 0, h = 0;
+    if (sscanf(e, "%dx%d", &w, &h) == 2 && w >= 1 && h >= 1 && w <= cfg->L && h <= cfg->L && w * h <= 1024) {
+      c->TW = w;
+      c->TH = h;
+    }
+  }
   c->tiles_x = (cfg->L + c->TW - 1) / c->TW;
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
   c->apt = (c->TW * c->TH + kBlock - 1) / kBlock <= 2 ? 2 : 4;
   const int HA = cfg->second_order ? 2 : 1;
-  c->lds_bytes = (size_t)lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA).bytes;
-  if (c->lds_bytes > 160 * 1024) {
+  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA);
+  c->lds_bytes = (size_t)ly.bytes;
+  // stage_region's per-thread register window must cover the S and R halos
+  const int js = cfg->second_order ? 8 : 7, jr = cfg->second_order ? 8 : 6;
+  if (c->lds_bytes > 160 * 1024 || ly.sw * ly.sh > js * kBlock || ly.rw * ly.rh > jr * kBlock) {
     delete c;
     return SPGG_E_ARG;
   }

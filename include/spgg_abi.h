@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 2
+#define SPGG_ABI_VERSION 3
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -84,7 +84,8 @@ typedef struct {
   int32_t state_mode;    /* SPGG_STATE_* */
   int32_t rng_mode;      /* SPGG_RNG_* */
   int32_t iterations;    /* capacity: stats/eps tables hold iterations+2 slots */
-  int32_t reserved;
+  int32_t rep_int8;      /* 1: R buffers hold int8 multiples of each replica's rep_unit
+                            (exact when gains/bounds are dyadic multiples, see below) */
 } spgg_config;
 
 /* Per-replica constants, precomputed by the host in the reference's own
@@ -113,6 +114,13 @@ typedef struct {
    * the host in the reference's order. */
   double pay_c[6];
   double pay_d[6];
+  /* compact reputation (spgg_config.rep_int8): R = k*rep_unit with
+   * k in [rk_min, rk_max] (int8); gain/loss per action in the same units.
+   * Valid only when rep_gain_C, delta_R_D, R_min, R_max are all exact
+   * multiples of a dyadic rep_unit: then every f64 sum/clip of the reference
+   * is exact and the int8 path reproduces it bit for bit. */
+  double rep_unit;
+  int32_t rk_gain, rk_loss, rk_min, rk_max;
 } spgg_rep_params;
 
 /* Device buffers, all replica-major.  n = L*L.  Ping-pong pairs are indexed
@@ -120,7 +128,7 @@ typedef struct {
  *   S[2]      uint8  [n_rep][n]      bit0: strategy S_t (0 = C); bits 1-3: the
  *                                    deferred-NI record of iteration t-1
  *                                    (s_old, a*==a, prev strategy)
- *   R[2]      f64    [n_rep][n]      reputation R_t
+ *   R[2]      f64    [n_rep][n]      reputation R_t (int8 R_t/rep_unit if rep_int8)
  *   Q[2]      f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2);
  *                                    Q[(t-1)&1] holds iteration t-1's TD update
  *                                    without its NI term (applied by iteration t)
@@ -140,7 +148,7 @@ typedef struct {
  */
 typedef struct {
   uint8_t* S[2];
-  double* R[2];
+  void* R[2];     /* double, or int8_t when spgg_config.rep_int8 */
   double* Q[2];
   double* md[2];
   float* atd;

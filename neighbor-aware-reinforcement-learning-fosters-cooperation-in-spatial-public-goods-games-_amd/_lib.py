@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -36,7 +36,7 @@ class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("n_rep", ctypes.c_int32), ("L", ctypes.c_int32),
                 ("second_order", ctypes.c_int32), ("state_mode", ctypes.c_int32),
                 ("rng_mode", ctypes.c_int32), ("iterations", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("rep_int8", ctypes.c_int32)]
 
 
 class RepParams(ctypes.Structure):
@@ -44,7 +44,10 @@ class RepParams(ctypes.Structure):
         "rc", "cost", "norm_min", "norm_den", "w_p", "w_rep", "alpha", "gamma",
         "diag_alpha", "diag_gamma", "kappa", "lambda_eps", "rep_gain_c", "neg_delta_r_d",
         "r_min", "r_max")] + [("seed", ctypes.c_uint64), ("reserved", ctypes.c_uint64),
-                              ("pay_c", ctypes.c_double * 6), ("pay_d", ctypes.c_double * 6)]
+                              ("pay_c", ctypes.c_double * 6), ("pay_d", ctypes.c_double * 6),
+                              ("rep_unit", ctypes.c_double), ("rk_gain", ctypes.c_int32),
+                              ("rk_loss", ctypes.c_int32), ("rk_min", ctypes.c_int32),
+                              ("rk_max", ctypes.c_int32)]
 
 
 class Buffers(ctypes.Structure):

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,8 +55,8 @@ constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
 struct TileArgs {
   const uint8_t* S_in;  // S_t   (bit0 strategy, bits1-3 pending-NI bookkeeping)
   uint8_t* S_out;       // S_{t+1}
-  const double* R_in;
-  double* R_out;
+  const void* R_in;     // f64, or int8 units of rep_unit (compact reputation)
+  void* R_out;
   const double* Q_in;   // [rep][n][4]: after TD of t-1, before its NI term
   double* Q_out;
   const double* md_in;  // max(0, max_diff) of t-1
@@ -75,16 +76,16 @@ struct LdsLayout {
   int off_R, off_Rn, off_Rew, off_S, off_A, bytes;
 };
 
-// f64 arrays first (16-byte aligned carve), then bytes.
-__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HR, int HA) {
+// 16-byte aligned carve: f64 first, then the R planes (rsz = 8 or 1), then bytes.
+__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HR, int HA, int rsz) {
   LdsLayout l;
   l.sw = tw + 2 * HS; l.sh = th + 2 * HS;
   l.rw = tw + 2 * HR; l.rh = th + 2 * HR;
   l.aw = tw + 2 * HA; l.ah = th + 2 * HA;
   int off = (12 + kWaves * 64) * 8;  // payoff table + reduction scratch
-  l.off_R = off;   off += ((l.rw * l.rh * 8 + 15) / 16) * 16;
-  l.off_Rn = off;  off += ((l.aw * l.ah * 8 + 15) / 16) * 16;
   l.off_Rew = off; off += ((l.aw * l.ah * 8 + 15) / 16) * 16;
+  l.off_R = off;   off += ((l.rw * l.rh * rsz + 15) / 16) * 16;
+  l.off_Rn = off;  off += ((l.aw * l.ah * rsz + 15) / 16) * 16;
   l.off_S = off;   off += ((l.sw * l.sh + 15) / 16) * 16;
   l.off_A = off;   off += ((l.aw * l.ah + 15) / 16) * 16;
   l.bytes = off;
@@ -102,6 +103,35 @@ __device__ __forceinline__ Cells13 cells_at(const uint8_t* s, int c, int w) {
   r.cM0 = CO(-2 * w); r.cP0 = CO(2 * w); r.c0M = CO(-2); r.c0P = CO(2);
 #undef CO
   return r;
+}
+
+// Compact reputation: when rep_gain_C, delta_R_D, R_min, R_max are multiples
+// of a dyadic unit u with |R/u| <= 127 (host-checked), every R the reference
+// can produce is k*u exactly, its f64 sums and clip are exact, and
+// (sum/n > 0) <=> (sum of k > 0): int8 storage is bit-identical.
+template <bool RQ>
+using RStore = typename std::conditional<RQ, int8_t, double>::type;
+template <bool RQ>
+using RVal = typename std::conditional<RQ, int, double>::type;
+
+template <bool RQ>
+__device__ __forceinline__ RVal<RQ> rep_next(RVal<RQ> r, int act, const spgg_rep_params& p) {
+  if constexpr (RQ) {  // spgg.py:321-323 in units of rep_unit
+    const int k = r + (act == 0 ? p.rk_gain : -p.rk_loss);
+    return min(max(k, p.rk_min), p.rk_max);
+  } else {             // spgg.py:321-323
+    const double x = r + (act == 0 ? p.rep_gain_c : p.neg_delta_r_d);
+    return fmin(fmax(x, p.r_min), p.r_max);
+  }
+}
+
+template <bool M2>
+__device__ __forceinline__ int rep_state_lds(const int8_t* R, int c, int w) {
+  int acc = R[c] + R[c - w] + R[c + w] + R[c - 1] + R[c + 1];
+  if constexpr (M2)
+    acc += R[c - 2 * w] + R[c + 2 * w] + R[c - 2] + R[c + 2] + R[c - w - 1] + R[c - w + 1] + R[c + w - 1] +
+           R[c + w + 1];
+  return acc > 0 ? 1 : 0;
 }
 
 // Reputation sum in the reference's offset order (spgg.py:296-305):
@@ -193,8 +223,9 @@ __device__ __forceinline__ double rcp_diag(double x) {
 enum { C_SWCD = 0, C_SWDC = 8, C_NCOOP1 = 16, C_NMD = 24 };   // cnt0
 enum { C_NMD2 = 0, C_GC0 = 8 };                                // cnt1: GC0..2 at 8,16,24; cnt2: GC3..5
 
-template <bool M2, bool AS, int RNG, int APT>
+template <bool M2, bool AS, bool RQ, int RNG, int APT>
 __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
+  using RT = RStore<RQ>;
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
   constexpr int HR = 2 * HA;      // R_t halo: states of ring agents
   constexpr int HS = HA + 2;      // S_t halo: payoffs of ring agents
@@ -216,11 +247,13 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   const int tyi = tile / a.tiles_x, txi = tile - (tile / a.tiles_x) * a.tiles_x;
   const int y0 = tyi * a.TH, x0 = txi * a.TW;
   const int th = min(a.TH, L - y0), tw = min(a.TW, L - x0);
-  const LdsLayout ly = lds_layout(tw, th, HS, HR, HA);
+  const LdsLayout ly = lds_layout(tw, th, HS, HR, HA, (int)sizeof(RT));
   double* tab = reinterpret_cast<double*>(smem);
   double* red = tab + 12;
-  double* sR = reinterpret_cast<double*>(smem + ly.off_R);
-  double* sRn = reinterpret_cast<double*>(smem + ly.off_Rn);
+  RT* sR = reinterpret_cast<RT*>(smem + ly.off_R);
+  RT* sRn = reinterpret_cast<RT*>(smem + ly.off_Rn);
+  const RT* Rin = reinterpret_cast<const RT*>(a.R_in);
+  RT* Rout = reinterpret_cast<RT*>(a.R_out);
   double* sRew = reinterpret_cast<double*>(smem + ly.off_Rew);
   uint8_t* sS = smem + ly.off_S;
   uint8_t* sA = smem + ly.off_A;
@@ -281,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   }
   if (tid < 12) tab[tid] = tid < 6 ? pg.pay_c[tid] : pg.pay_d[tid - 6];
   stage_region<(M2 ? 8 : 7)>(sS, a.S_in + rb, ly.sh, ly.sw, y0 - HS, x0 - HS, L, tiny);
-  if (!AS && !fin_only) stage_region<(M2 ? 8 : 6)>(sR, a.R_in + rb, ly.rh, ly.rw, y0 - HR, x0 - HR, L, tiny);
+  if (!AS && !fin_only) stage_region<(M2 ? 8 : 6)>(sR, Rin + rb, ly.rh, ly.rw, y0 - HR, x0 - HR, L, tiny);
   __syncthreads();
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
@@ -335,11 +368,11 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     const int cs = (r + HS) * ly.sw + (c + HS);
     const int s_t = sS[cs] & 1;
     const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
-    const double r_t = AS ? a.R_in[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
+    const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
     const double cmask = s_t ? 0.0 : 1.0;
     va[0] += P;                                           // spgg.py:388-390
     va[1] += P * cmask;
-    va[2] += r_t;                                         // spgg.py:394
+    va[2] += (double)r_t;                                 // spgg.py:394 (units if RQ)
     if (!acting) continue;
     int so;                                               // spgg.py:409
     if constexpr (AS) so = s_t == 0 ? 1 : 0;
@@ -357,16 +390,15 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     }
     const double qs0 = so ? q[u][2] : q[u][0], qs1 = so ? q[u][3] : q[u][1];
     const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);    // argmax ties -> 0
-    double rn = r_t + (act == 0 ? pg.rep_gain_c : pg.neg_delta_r_d);  // spgg.py:321-323
-    rn = fmin(fmax(rn, pg.r_min), pg.r_max);
+    const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
     const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
     const double wpp = w_p * P, wrr = w_rep * rr;
     const double rew = wpp + wrr;
     const int ca = (r + HA) * ly.aw + (c + HA);
     sA[ca] = (uint8_t)act;
-    sRn[ca] = rn;
+    sRn[ca] = (RT)rn;
     sRew[ca] = rew;
-    a.R_out[rb + gidx[u]] = rn;
+    Rout[rb + gidx[u]] = (RT)rn;
     own_bits[u] = act | (so << 1) | (s_t << 3);
     cnt0 += ((s_t == 0 && act == 1) ? 1u : 0u) << C_SWCD;  // spgg.py:419-420
     cnt0 += ((s_t == 1 && act == 0) ? 1u : 0u) << C_SWDC;
@@ -408,10 +440,10 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       if (pending) apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den);
       const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
       int so;
-      double r_t;
+      RVal<RQ> r_t;
       if constexpr (AS) {
         so = s_t == 0 ? 1 : 0;
-        r_t = 0.0;  // R of ring agents is not needed in action-state mode
+        r_t = 0;  // R of ring agents is not needed in action-state mode
       } else {
         const int cr = (ay + (HR - HA)) * ly.rw + (ax + (HR - HA));
         so = rep_state_lds<M2>(sR, cr, ly.rw);
@@ -430,12 +462,11 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       }
       const double qs0 = so ? qq[2] : qq[0], qs1 = so ? qq[3] : qq[1];
       const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);
-      double rn = r_t + (act == 0 ? pg.rep_gain_c : pg.neg_delta_r_d);
-      rn = fmin(fmax(rn, pg.r_min), pg.r_max);
+      const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
       const double rew = w_p * P + w_rep * (act == 0 ? 0.5 : 0.0);
       const int ca = ay * ly.aw + ax;
       sA[ca] = (uint8_t)act;
-      sRn[ca] = rn;
+      sRn[ca] = (RT)rn;
       sRew[ca] = rew;
     }
   }
@@ -556,7 +587,8 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         tot[0] += red[w * 64 + src];
         if (src_c >= 0) tot[1] += red[w * 64 + src_c];
       }
-      const double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
+      double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
+      if (RQ && k == SPGG_ST_SUMR) val *= pg.rep_unit;
       if (val != 0.0 && (!(SPGG_ABLATE & 2) || k == SPGG_ST_NCOOP))
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);
     }
@@ -755,20 +787,23 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   return a;
 }
 
-template <bool M2, bool AS, int RNG>
+template <bool M2, bool AS, bool RQ, int RNG>
 void launch_step_t(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
   const int total = c->cfg.n_rep * c->tiles_per_rep;
   const dim3 grid(((total + 7) / 8) * 8);
-  if (c->apt <= 2)
-    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RNG, 2>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
-  else
-    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RNG, 4>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
+  hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 4>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
+}
+
+template <bool M2, bool AS, bool RQ>
+void launch_step_rng(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (c->cfg.rng_mode == SPGG_RNG_PHILOX) launch_step_t<M2, AS, RQ, SPGG_RNG_PHILOX>(c, a, t, fin, s);
+  else launch_step_t<M2, AS, RQ, SPGG_RNG_MT19937>(c, a, t, fin, s);  // INJECT reads the same bytes
 }
 
 template <bool M2, bool AS>
-void launch_step_rng(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
-  if (c->cfg.rng_mode == SPGG_RNG_PHILOX) launch_step_t<M2, AS, SPGG_RNG_PHILOX>(c, a, t, fin, s);
-  else launch_step_t<M2, AS, SPGG_RNG_MT19937>(c, a, t, fin, s);  // INJECT reads the same bytes
+void launch_step_rq(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (c->cfg.rep_int8) launch_step_rng<M2, AS, true>(c, a, t, fin, s);
+  else launch_step_rng<M2, AS, false>(c, a, t, fin, s);
 }
 
 void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
@@ -776,11 +811,11 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   const bool m2 = c->cfg.second_order != 0;
   const bool as = c->cfg.state_mode == SPGG_STATE_ACTION;
   if (m2) {
-    if (as) launch_step_rng<true, true>(c, a, t, fin, s);
-    else launch_step_rng<true, false>(c, a, t, fin, s);
+    if (as) launch_step_rq<true, true>(c, a, t, fin, s);
+    else launch_step_rq<true, false>(c, a, t, fin, s);
   } else {
-    if (as) launch_step_rng<false, true>(c, a, t, fin, s);
-    else launch_step_rng<false, false>(c, a, t, fin, s);
+    if (as) launch_step_rq<false, true>(c, a, t, fin, s);
+    else launch_step_rq<false, false>(c, a, t, fin, s);
   }
 }
 
@@ -822,7 +857,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
   c->apt = (c->TW * c->TH + kBlock - 1) / kBlock <= 2 ? 2 : 4;
   const int HA = cfg->second_order ? 2 : 1;
-  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA);
+  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA, cfg->rep_int8 ? 1 : 8);
   c->lds_bytes = (size_t)ly.bytes;
   // stage_region's per-thread register window must cover the S and R halos
   const int js = cfg->second_order ? 8 : 7, jr = cfg->second_order ? 8 : 6;

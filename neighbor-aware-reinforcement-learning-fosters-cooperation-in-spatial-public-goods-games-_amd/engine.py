@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import math
+import os
 from typing import Callable, Optional, Sequence
 
 import numpy as np
@@ -78,7 +80,37 @@ class ReplicaParams:
             tk = rc * N / 5
             p.pay_c[N] = float(tk - self.cost)
             p.pay_d[N] = float(tk)
+        u = self.rep_unit()
+        if u is not None:
+            p.rep_unit = u
+            p.rk_gain = int(self.rep_gain_C / u)
+            p.rk_loss = int(self.delta_R_D / u)
+            p.rk_min = int(self.R_min / u)
+            p.rk_max = int(self.R_max / u)
         return p
+
+    def rep_unit(self):
+        """Dyadic unit u (1, 1/2, ..., 1/1024) such that rep_gain_C, delta_R_D,
+        R_min, R_max are exact multiples of u with every reachable R/u in int8,
+        or None.  Then R = k*u exactly for every R the reference produces
+        (R starts at 0, spgg.py:129; updates spgg.py:321-323 stay exact), so
+        the int8 lattice reproduces the f64 one bit for bit."""
+        vals = [self.rep_gain_C, self.delta_R_D, self.R_min, self.R_max]
+        try:
+            vals = [float(v) for v in vals]
+        except (TypeError, ValueError):
+            return None
+        if not all(math.isfinite(v) for v in vals) or vals[2] > vals[3] or vals[2] > 0 or vals[3] < 0:
+            return None
+        for m in range(11):
+            u = 2.0 ** -m
+            ks = [v / u for v in vals]
+            if all(k == int(k) for k in ks):
+                g, l_, lo, hi = (int(k) for k in ks)
+                if -128 <= lo and hi <= 127 and abs(g) <= 127 and abs(l_) <= 127:
+                    return u
+                return None
+        return None
 
 
 def epsilon_table(eps0, decay, emin, n):
@@ -152,7 +184,11 @@ class BatchEngine:
         Q0 = np.stack([np.asarray(s.Q, dtype=np.float64).reshape(n, 4) for s in self.init])
         self.S = torch.zeros((2, R, n), dtype=u8, device=d)
         self.S[0].copy_(torch.from_numpy(S0))
-        self.Rep = torch.zeros((2, R, n), dtype=f64, device=d)
+        units = [p.rep_unit() for p in self.reps]
+        self.rep_int8 = (all(u is not None for u in units)
+                         and os.environ.get("SPGG_REP_F64", "0") != "1")
+        self.rep_units = np.array([u if u is not None else 1.0 for u in units])
+        self.Rep = torch.zeros((2, R, n), dtype=torch.int8 if self.rep_int8 else f64, device=d)
         self.Qb = torch.zeros((2, R, n, 4), dtype=f64, device=d)
         self.Qb[0].copy_(torch.from_numpy(Q0))
         self.md = torch.zeros((2, R, n), dtype=f64, device=d)
@@ -185,7 +221,7 @@ class BatchEngine:
     def _create(self):
         cfg = C.Config(device=self.dev.index, n_rep=self.R, L=self.L, second_order=int(self.M2),
                        state_mode=C.STATE_ACTION if self.state_rep == "action" else C.STATE_REPUTATION,
-                       rng_mode=C.RNG_MODES[self.rng], iterations=self.T, reserved=0)
+                       rng_mode=C.RNG_MODES[self.rng], iterations=self.T, rep_int8=int(self.rep_int8))
         ctx = ctypes.c_void_p()
         C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
         self.ctx = ctx
@@ -293,7 +329,7 @@ class BatchEngine:
         stop = self.stop_iter.cpu().numpy()
         cur = (t - 1) & 1
         S = self.S[cur].cpu().numpy() & 1
-        Rn = self.Rep[cur].cpu().numpy() if snap else None
+        Rn = self._rep_host(cur) if snap else None
         for k in range(self.R):
             if stop[k] != 0:
                 continue
@@ -319,9 +355,16 @@ class BatchEngine:
             cur, qb = last & 1, (last + 1) & 1
         L = self.L
         Q = self.Qb[qb, k].cpu().numpy().reshape(L, L, 2, 2)
-        R = self.Rep[cur, k].cpu().numpy().reshape(L, L)
+        R = self._rep_host(cur)[k].reshape(L, L)
         S = (self.S[cur, k].cpu().numpy() & 1).reshape(L, L).astype(np.int64)
         return Q, R, S
+
+    def _rep_host(self, buf):
+        """R plane `buf` of every replica as float64 (exact k*unit in compact mode)."""
+        x = self.Rep[buf].cpu().numpy()
+        if self.rep_int8:
+            return x.astype(np.float64) * self.rep_units[:, None]
+        return x
 
     def payoff_at(self, t):
         """P from S_t for every replica (device kernel), as (R, L, L) float64."""

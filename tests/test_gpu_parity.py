@@ -165,3 +165,26 @@ def test_philox_mode_deterministic_and_sane():
         assert np.all((cr >= 0) & (cr <= 1))
         # identical eps schedule to the reference
         assert h["epsilon_history_final"][0] == max(0.5 * 0.99, 0.01)
+
+
+@pytest.mark.parametrize("name", ["m1_rep_L16", "m2_rep_L24_stopC", "defaults_L12", "m2_act_L13_odd"])
+def test_spgg_dropin_f64_reputation_path(name, tmp_path, monkeypatch):
+    """Same fixtures with the compact int8 reputation disabled (f64 R planes)."""
+    monkeypatch.setenv("SPGG_REP_F64", "1")
+    test_spgg_dropin_matches_reference(name, tmp_path)
+
+
+@pytest.mark.parametrize("gain,loss,rmin,rmax", [(0.3, 1.0, -10, 10), (1.0, 0.7, -5.5, 3.25), (0.25, 0.5, -1, 1)])
+def test_nondyadic_and_dyadic_reputation_vs_oracle(gain, loss, rmin, rmax):
+    L, T = 24, 80
+    reps = [_runner_params(seed=s, rep_gain_C=gain, delta_R_D=loss, R_min=rmin, R_max=rmax) for s in (3, 4)]
+    eng = BatchEngine(L, T, reps, use_second_order=True, rng="mt19937")
+    assert eng.rep_int8 == (reps[0].rep_unit() is not None)
+    eng.run(snapshots=False)
+    for k, p in enumerate(reps):
+        ds, fin = _oracle_final(L, T, p, p.seed, True, "reputation")
+        Q, R, S = eng.final_state(k)
+        assert np.array_equal(Q, fin["Q"]) and np.array_equal(R, fin["R"]) and np.array_equal(S, fin["S"])
+        np.testing.assert_allclose(eng.histories()[k]["rep_avg_history_final"], ds["rep_avg_history_final"],
+                                   **FLOAT_TOL)
+    eng.close()

@@ -7,7 +7,7 @@ echo "== ablations (cfg3 philox)"
 echo -n "full      : "; timeout -k 10 120 $B | ms || exit 1
 for m in 1 2 4 7; do echo -n "ablate$m   : "; SPGG_LIB=build_ablate/libspgg_ablate$m.so timeout -k 10 120 $B | ms || exit 1; done
 echo "== tile shapes"
-for tl in 40x25 50x20 25x40 32x32 64x16 20x20 32x16 16x16; do echo -n "$tl: "; SPGG_TILE=$tl timeout -k 10 120 $B | ms || exit 1; done
+for tl in 40x25 50x20 40x20 32x32 64x16 20x20; do echo -n "$tl: "; SPGG_TILE=$tl timeout -k 10 120 $B | ms || exit 1; done
 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
 cd /tmp
 P="rocprofv3 --output-format csv --kernel-trace"

@@ -1,0 +1,98 @@
+"""Replica sharding across GPUs: one process per GPU, RCCL only for the final gather.
+
+Replicas (independent (r, kappa, seed, ...) lattices) never exchange data
+during a run, so a sweep is sharded as contiguous blocks of the replica list
+(the reference's only parallelism is a process pool over experiments,
+src/experiments/runner.py:136-154).  At the end every rank all-gathers the
+per-replica summaries (final cooperation rate etc.) — one collective of a few
+KB-MB over xGMI, latency-bound, never per step.
+
+Works with any torch.distributed backend: "nccl" (RCCL on ROCm) for GPU
+tensors, "gloo" for the CPU tests.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+import torch
+
+
+def shard_range(n_items: int, world: int, rank: int):
+    """[start, stop) of rank's contiguous block; block sizes differ by at most one."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} for world size {world}")
+    base, extra = divmod(n_items, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def shard(items: Sequence, world: int, rank: int):
+    a, b = shard_range(len(items), world, rank)
+    return list(items[a:b])
+
+
+def gather_rows(local: np.ndarray, n_items: int, device=None, group=None) -> np.ndarray:
+    """All-gather each rank's (k_rank, m) float64 block back into (n_items, m), in replica order.
+
+    Blocks are padded to the largest shard so a single fixed-size all_gather
+    suffices (no object pickling)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = shard_range(n_items, world, rank)
+    local = np.asarray(local, dtype=np.float64)
+    if local.ndim == 1:
+        local = local[:, None]
+    if local.shape[0] != b - a:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, shard is {b - a}")
+    m = local.shape[1]
+    rows = max(shard_range(n_items, world, r)[1] - shard_range(n_items, world, r)[0] for r in range(world))
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    buf = torch.zeros((rows, m), dtype=torch.float64, device=dev)
+    if b > a:
+        buf[: b - a] = torch.from_numpy(local).to(dev)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    out = np.empty((n_items, m))
+    for r in range(world):
+        ra, rb_ = shard_range(n_items, world, r)
+        out[ra:rb_] = parts[r][: rb_ - ra].cpu().numpy()
+    return out
+
+
+SUMMARY_FIELDS = ("final_coop", "final_def", "stop_iter", "iterations_run")
+
+
+def replica_summaries(engine) -> np.ndarray:
+    """(R, 4) float64 per-replica summary of a finished BatchEngine."""
+    out = np.zeros((engine.R, len(SUMMARY_FIELDS)))
+    for k in range(engine.R):
+        _, _, S = engine.final_state(k)
+        n = S.size
+        c = float(np.sum(S == 0)) / n
+        out[k] = (c, 1.0 - c, float(engine.stopped[k]), float(engine.last_iteration(k)))
+    return out
+
+
+def run_sharded(replicas, L: int, iterations: int, use_second_order=True,
+                state_representation="reputation", rng="mt19937", device=None, group=None):
+    """Run this rank's block of `replicas` on its GPU, then all-gather the summaries.
+
+    Returns (summaries (N, 4) on every rank, this rank's BatchEngine)."""
+    import torch.distributed as dist
+    from .engine import BatchEngine
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    mine = shard(replicas, world, rank)
+    eng = None
+    local = np.zeros((0, len(SUMMARY_FIELDS)))
+    if mine:
+        eng = BatchEngine(L, iterations, mine, use_second_order=use_second_order,
+                          state_representation=state_representation, rng=rng, device=device)
+        eng.run(snapshots=False)
+        local = replica_summaries(eng)
+    if world == 1:
+        return local, eng
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else None
+    return gather_rows(local, len(replicas), device=dev, group=group), eng

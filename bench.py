@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--rng", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--streams", type=int, default=None,
+                    help="replica groups on concurrent HIP streams (default: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
@@ -128,7 +130,8 @@ def main():
     desc, L, M2, state, reps = workload(args.config, rank)
     K, W = args.steps, args.warmup
     T = K + W
-    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng)
+    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng,
+                      streams=args.streams)
     n_agents = len(reps) * L * L
 
     eng.step(W)
@@ -182,7 +185,8 @@ def main():
             "data": "synthetic (reference init: S~Bernoulli(1/2), R=0, Q~U(-0.01,0.01))",
             "config": {"workload": desc, "L": L, "replicas_per_gpu": len(reps),
                        "agents_per_gpu": n_agents, "second_order": M2, "state": state,
-                       "rng": args.rng, "parallelism": f"replicas sharded over {world} GPU(s)"},
+                       "rng": args.rng, "streams_per_gpu": eng.G,
+                       "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "spgg_step_kernel (one launch per iteration)" if args.rng == "philox" else "spgg_mt_draw_kernel + spgg_step_kernel",

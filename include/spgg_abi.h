@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 3
+#define SPGG_ABI_VERSION 5
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -108,7 +108,7 @@ typedef struct {
   double r_min;
   double r_max;
   uint64_t seed;      /* Philox key (SPGG_RNG_PHILOX only) */
-  uint64_t reserved;
+  uint64_t stream_id; /* Philox stream: global replica id (independent of batching) */
   /* group payoff of a cooperator / defector in a group with N cooperators,
    * N = 0..5: (r*c*N)/5 - cost and (r*c*N)/5 (spgg.py:256-257), computed by
    * the host in the reference's order. */
@@ -121,6 +121,7 @@ typedef struct {
    * is exact and the int8 path reproduces it bit for bit. */
   double rep_unit;
   int32_t rk_gain, rk_loss, rk_min, rk_max;
+  double norm_rcp;    /* 1/norm_den rounded to nearest (host) */
 } spgg_rep_params;
 
 /* Device buffers, all replica-major.  n = L*L.  Ping-pong pairs are indexed

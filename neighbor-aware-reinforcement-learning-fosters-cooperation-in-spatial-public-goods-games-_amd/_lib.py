@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 5
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -43,11 +43,11 @@ class RepParams(ctypes.Structure):
     _fields_ = [(name, ctypes.c_double) for name in (
         "rc", "cost", "norm_min", "norm_den", "w_p", "w_rep", "alpha", "gamma",
         "diag_alpha", "diag_gamma", "kappa", "lambda_eps", "rep_gain_c", "neg_delta_r_d",
-        "r_min", "r_max")] + [("seed", ctypes.c_uint64), ("reserved", ctypes.c_uint64),
+        "r_min", "r_max")] + [("seed", ctypes.c_uint64), ("stream_id", ctypes.c_uint64),
                               ("pay_c", ctypes.c_double * 6), ("pay_d", ctypes.c_double * 6),
                               ("rep_unit", ctypes.c_double), ("rk_gain", ctypes.c_int32),
                               ("rk_loss", ctypes.c_int32), ("rk_min", ctypes.c_int32),
-                              ("rk_max", ctypes.c_int32)]
+                              ("rk_max", ctypes.c_int32), ("norm_rcp", ctypes.c_double)]
 
 
 class Buffers(ctypes.Structure):
@@ -61,17 +61,19 @@ class SpggError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
 _lock = threading.Lock()
 
 
 def load(path: str | None = None):
-    """Load (once) and type the shared library; raises if it is absent."""
-    global _lib
+    """Load (once per path) and type the shared library; raises if it is absent.
+
+    `path` / $SPGG_LIB select a tuning build (A/B timing); each path gets its
+    own RTLD_LOCAL handle, so variants can coexist in one process."""
     with _lock:
-        if _lib is not None:
-            return _lib
-        p = path or os.environ.get("SPGG_LIB") or LIB_PATH  # SPGG_LIB: tuning builds only
+        p = path or os.environ.get("SPGG_LIB") or LIB_PATH
+        if p in _libs:
+            return _libs[p]
         if not os.path.exists(p):
             raise SpggError(f"{p} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
         lib = ctypes.CDLL(p)
@@ -101,12 +103,12 @@ def load(path: str | None = None):
         v = lib.spgg_abi_version()
         if v != ABI_VERSION:
             raise SpggError(f"libspgg_hip ABI {v} != expected {ABI_VERSION}")
-        _lib = lib
+        _libs[p] = lib
         return lib
 
 
-def check(rc: int, ctx=None, what: str = ""):
+def check(rc: int, ctx=None, what: str = "", lib=None):
     if rc != OK:
-        lib = load()
+        lib = lib or load()
         detail = lib.spgg_last_error(ctx).decode() if ctx else ""
         raise SpggError(f"{what} failed (rc={rc}): {detail}")

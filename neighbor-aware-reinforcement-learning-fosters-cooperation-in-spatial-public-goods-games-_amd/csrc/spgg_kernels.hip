@@ -159,9 +159,9 @@ __device__ __forceinline__ int rep_state_lds(const double* R, int c, int w) {
 
 // Deferred NI of iteration t-1 on one agent's Q (spgg.py:489-509).
 __device__ __forceinline__ double apply_pending(double (&q)[4], uint8_t b, double md, double kappa,
-                                                double lam_den) {
+                                                double lam_den, double lam_rcp) {
   const int e = ((b >> 1) & 1) * 2 + (b & 1);  // (s_old, a) of iteration t-1
-  const double lam = (kappa * md) / lam_den;
+  const double lam = div_uniform(kappa * md, lam_den, lam_rcp);  // (kappa*max(0,md))/(gmax+eps)
   const double nu = lam * (((b >> 2) & 1) ? 1.0 : -1.0);
   q_set(q, e, q_get(q, e) + nu);
   return nu;
@@ -185,8 +185,10 @@ __device__ __forceinline__ int wrap1(int x, int L, bool tiny) {
 }
 
 // Copy an h x w window of a periodic L x L plane (origin y0, x0; may wrap)
-// into LDS.  Every global load of the thread is issued before the first LDS
-// store, so the whole window costs one memory round trip (J >= h*w/kBlock).
+// into LDS, flattened over all 256 threads.  Every global load of the thread
+// is issued before the first LDS store: one memory round trip
+// (J >= h*w/kBlock; host-checked).  Measured 5% faster than one-row-per-wave
+// staging (lane-constant columns but 28% idle lanes at 46-wide rows).
 template <int J, typename T>
 __device__ __forceinline__ void stage_region(T* dst, const T* src, int h, int w, int y0, int x0, int L,
                                              bool tiny) {
@@ -270,11 +272,13 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   const bool acting = !fin_only && !stop_now;
   const bool pending = t > 1;
   const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
+  const double lam_rcp = 1.0 / lam_den;  // IEEE, once per workgroup
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
   const size_t rb = (size_t)rep * n;
   const int tid = threadIdx.x;
-  // Philox key: 64-bit seed folded with the replica index (distinct streams per replica)
-  const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^ (uint32_t)rep * 0xC2B2AE35u;
+  // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
+  const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
+                        (uint32_t)pg.stream_id * 0xC2B2AE35u;
 
   // ---- phase 0: owned-agent registers + LDS staging ----------------------
   // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         if (gidx[u] < 0) continue;
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
-        const double nu = apply_pending(q[u], b, md_own[u], kappa, lam_den);
+        const double nu = apply_pending(q[u], b, md_own[u], kappa, lam_den, lam_rcp);
         const double anu = fabs(nu);
         v[0] += (anu * rcp_diag(((double)atd_own[u] + anu) + 1e-8)) * 100.0;  // spgg.py:512
         const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                        // prev_S of t-1 == C
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     const int r = rc[u] >> 16, c = rc[u] & 0xffff;
     const int cs = (r + HS) * ly.sw + (c + HS);
     const int s_t = sS[cs] & 1;
-    const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
+    const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
     const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
     const double cmask = s_t ? 0.0 : 1.0;
     va[0] += P;                                           // spgg.py:388-390
@@ -437,8 +441,8 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + g) * 4);
       const double2 q01 = qp[0], q23 = qp[1];
       double qq[4] = {q01.x, q01.y, q23.x, q23.y};
-      if (pending) apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den);
-      const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den);
+      if (pending) apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den, lam_rcp);
+      const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
       int so;
       RVal<RQ> r_t;
       if constexpr (AS) {
@@ -708,7 +712,7 @@ __global__ __launch_bounds__(kBlock) void spgg_payoff_kernel(const uint8_t* S, c
   c.cmm = CO(im1, jm1); c.cmp = CO(im1, jp1); c.cpm = CO(ip1, jm1); c.cpp = CO(ip1, jp1);
   c.cM0 = CO(im2, j); c.cP0 = CO(ip2, j); c.c0M = CO(i, jm2); c.c0P = CO(i, jp2);
 #undef CO
-  out[(size_t)rep * n + idx] = payoff13(c, tab, params[rep].norm_min, params[rep].norm_den);
+  out[(size_t)rep * n + idx] = payoff13(c, tab, params[rep].norm_min, params[rep].norm_den, params[rep].norm_rcp);
 }
 
 }  // namespace
@@ -744,7 +748,7 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
 void choose_tile(int L, int* TW, int* TH) {
   int best_w = std::min(L, 32), best_h = std::min(L, 32);
   double best = 1e300;
-  for (int w = std::min(L, 16); w <= std::min(L, 64); ++w) {
+  for (int w = std::min(L, 16); w <= std::min(L, 56); ++w) {
     for (int h = 1; h <= std::min(L, 64); ++h) {
       if (w * h > 1024) break;
       const int tx = (L + w - 1) / w, ty = (L + h - 1) / h;
@@ -848,7 +852,8 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   choose_tile(cfg->L, &c->TW, &c->TH);
   if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;
-    if (sscanf(e, "%dx%d", &w, &h) == 2 && w >= 1 && h >= 1 && w <= cfg->L && h <= cfg->L && w * h <= 1024) {
+    if (sscanf(e, "%dx%d", &w, &h) == 2 && w >= 1 && h >= 1 && w <= std::min(cfg->L, 56) &&
+        h <= std::min(cfg->L, 64) && w * h <= 1024) {
       c->TW = w;
       c->TH = h;
     }

@@ -62,6 +62,7 @@ class ReplicaParams:
         norm_max, norm_min = 4 * r, r - 5                # spgg.py:148-149
         p.norm_min = float(norm_min)
         p.norm_den = float(norm_max - norm_min)          # spgg.py:377
+        p.norm_rcp = 1.0 / p.norm_den                    # correctly rounded (device: Markstein)
         p.w_p = float(self.reward_weight_payoff)
         p.w_rep = float(1 - self.reward_weight_payoff)   # spgg.py:108
         p.alpha = float(self.alpha if self.alg_alpha is None else self.alg_alpha)
@@ -146,7 +147,8 @@ class BatchEngine:
 
     def __init__(self, L: int, iterations: int, replicas: Sequence[ReplicaParams],
                  use_second_order: bool = True, state_representation: str = "reputation",
-                 rng: str = "mt19937", device=None, init: Optional[Sequence[InitState]] = None):
+                 rng: str = "mt19937", device=None, init: Optional[Sequence[InitState]] = None,
+                 lib_path: Optional[str] = None, streams: Optional[int] = None):
         if state_representation not in ("reputation", "action"):
             raise ValueError(f"Unknown state_representation: {state_representation}. "
                              f"Must be 'reputation' or 'action'")
@@ -154,7 +156,7 @@ class BatchEngine:
             raise ValueError(f"rng must be one of {sorted(C.RNG_MODES)}")
         if not torch.cuda.is_available():
             raise C.SpggError("BatchEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
-        self.lib = C.load()
+        self.lib = C.load(lib_path)
         self.L, self.n = int(L), int(L) * int(L)
         self.T = int(iterations)
         self.reps = list(replicas)
@@ -168,6 +170,12 @@ class BatchEngine:
         self.init = list(init)
         if len(self.init) != self.R:
             raise ValueError("one InitState per replica")
+        # Replica groups on separate HIP streams: their step kernels run
+        # concurrently, so one group's tail / compute phase overlaps another
+        # group's memory phase (a single launch moves in lockstep rounds).
+        if streams is None:
+            streams = int(os.environ.get("SPGG_STREAMS", "0")) or self._auto_streams()
+        self.G = 1 if rng == "inject" else max(1, min(int(streams), self.R))
         self._alloc()
         self._create()
         self.t = 1                 # next iteration to execute
@@ -175,6 +183,13 @@ class BatchEngine:
         self.snapshots = [dict() for _ in range(self.R)]
         self.png_frames = [dict() for _ in range(self.R)]
         self._flushed = False
+
+    def _auto_streams(self):
+        """~700 workgroups per group kernel (measured best on MI355X for cfg3); small
+        batches stay on one stream (cross-stream ordering costs more than it hides)."""
+        tw = min(self.L, 40)
+        tiles = -(-self.L // tw) * -(-self.L // min(self.L, 25))
+        return int(max(1, min(8, round(self.R * tiles / 700))))
 
     # -- setup ---------------------------------------------------------------
     def _alloc(self):
@@ -222,29 +237,56 @@ class BatchEngine:
         cfg = C.Config(device=self.dev.index, n_rep=self.R, L=self.L, second_order=int(self.M2),
                        state_mode=C.STATE_ACTION if self.state_rep == "action" else C.STATE_REPUTATION,
                        rng_mode=C.RNG_MODES[self.rng], iterations=self.T, rep_int8=int(self.rep_int8))
-        ctx = ctypes.c_void_p()
-        C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
-        self.ctx = ctx
-        arr = (C.RepParams * self.R)(*[p.to_c() for p in self.reps])
-        C.check(self.lib.spgg_set_params(self.ctx, arr), self.ctx, "spgg_set_params")
-        b = C.Buffers()
-        for i in range(2):
-            b.S[i], b.R[i] = self.S[i].data_ptr(), self.Rep[i].data_ptr()
-            b.Q[i], b.md[i] = self.Qb[i].data_ptr(), self.md[i].data_ptr()
-        b.atd = self.atd.data_ptr()
-        b.explore, b.rbit = self.explore.data_ptr(), self.rbit.data_ptr()
-        b.mt_state = self.mt_state.data_ptr()
-        b.eps, b.stats, b.stop_iter = self.eps.data_ptr(), self.stats.data_ptr(), self.stop_iter.data_ptr()
-        self._bufs = b
-        C.check(self.lib.spgg_bind(self.ctx, b), self.ctx, "spgg_bind")
+        params = [p.to_c() for p in self.reps]
+        for k, p in enumerate(params):
+            p.stream_id = k
+        self.groups = []
+        bounds = np.linspace(0, self.R, self.G + 1).round().astype(int)
+        for g in range(self.G):
+            r0, r1 = int(bounds[g]), int(bounds[g + 1])
+            cfg.n_rep = r1 - r0
+            ctx = ctypes.c_void_p()
+            C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
+            arr = (C.RepParams * (r1 - r0))(*params[r0:r1])
+            C.check(self.lib.spgg_set_params(ctx, arr), ctx, "spgg_set_params")
+            b = C.Buffers()   # the group's replica slice of every buffer
+            for i in range(2):
+                b.S[i], b.R[i] = self.S[i][r0].data_ptr(), self.Rep[i][r0].data_ptr()
+                b.Q[i], b.md[i] = self.Qb[i][r0].data_ptr(), self.md[i][r0].data_ptr()
+            b.atd = self.atd[r0].data_ptr()
+            b.explore, b.rbit = self.explore[r0].data_ptr(), self.rbit[r0].data_ptr()
+            b.mt_state = self.mt_state[r0].data_ptr()
+            b.eps, b.stats = self.eps[r0].data_ptr(), self.stats[r0].data_ptr()
+            b.stop_iter = self.stop_iter[r0].data_ptr()
+            C.check(self.lib.spgg_bind(ctx, b), ctx, "spgg_bind")
+            stream = torch.cuda.current_stream(self.dev) if self.G == 1 else torch.cuda.Stream(self.dev)
+            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, bufs=b, stream=stream))
+        self.ctx = self.groups[0]["ctx"]
         tw, th = ctypes.c_int32(), ctypes.c_int32()
         C.check(self.lib.spgg_tile_shape(self.ctx, ctypes.byref(tw), ctypes.byref(th)), self.ctx, "tile")
         self.tile = (tw.value, th.value)
 
+    def _enqueue(self, fn):
+        """Run fn(group, stream_handle) on every group's stream, ordered after the
+        current stream's prior work and before its later work."""
+        cur = torch.cuda.current_stream(self.dev)
+        if self.G == 1:
+            fn(self.groups[0], cur.cuda_stream)
+            return
+        for g in self.groups:
+            g["stream"].wait_stream(cur)
+        for g in self.groups:
+            fn(g, g["stream"].cuda_stream)
+        for g in self.groups:
+            cur.wait_stream(g["stream"])
+
     def close(self):
-        if getattr(self, "ctx", None):
-            self.lib.spgg_destroy(self.ctx)
-            self.ctx = None
+        for g in getattr(self, "groups", []):
+            if g.get("ctx"):
+                self.lib.spgg_destroy(g["ctx"])
+                g["ctx"] = None
+        self.groups = []
+        self.ctx = None
 
     def __del__(self):
         try:
@@ -284,7 +326,9 @@ class BatchEngine:
                 C.check(self.lib.spgg_step(self.ctx, self.t, 1, self.stream), self.ctx, "spgg_step")
                 self.t += 1
         else:
-            C.check(self.lib.spgg_step(self.ctx, self.t, n_steps, self.stream), self.ctx, "spgg_step")
+            t0 = self.t
+            self._enqueue(lambda g, s: C.check(self.lib.spgg_step(g["ctx"], t0, n_steps, s), g["ctx"],
+                                               "spgg_step"))
             self.t += n_steps
         return n_steps
 
@@ -296,7 +340,8 @@ class BatchEngine:
         """Apply the deferred NI term of the last executed iteration (once, at the end)."""
         if self._flushed or self.t <= 1:
             return
-        C.check(self.lib.spgg_flush(self.ctx, self.t - 1, self.stream), self.ctx, "spgg_flush")
+        tl = self.t - 1
+        self._enqueue(lambda g, s: C.check(self.lib.spgg_flush(g["ctx"], tl, s), g["ctx"], "spgg_flush"))
         self._flushed = True
 
     def run(self, chunk: int = 256, snapshots: bool = True, png: bool = False,
@@ -368,8 +413,8 @@ class BatchEngine:
 
     def payoff_at(self, t):
         """P from S_t for every replica (device kernel), as (R, L, L) float64."""
-        C.check(self.lib.spgg_payoff(self.ctx, int(t), self.P_buf.data_ptr(), self.stream),
-                self.ctx, "spgg_payoff")
+        self._enqueue(lambda g, s: C.check(
+            self.lib.spgg_payoff(g["ctx"], int(t), self.P_buf[g["r0"]].data_ptr(), s), g["ctx"], "spgg_payoff"))
         return self.P_buf.cpu().numpy().reshape(self.R, self.L, self.L)
 
     def mt_state_host(self, k):

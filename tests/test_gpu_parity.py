@@ -188,3 +188,24 @@ def test_nondyadic_and_dyadic_reputation_vs_oracle(gain, loss, rmin, rmax):
         np.testing.assert_allclose(eng.histories()[k]["rep_avg_history_final"], ds["rep_avg_history_final"],
                                    **FLOAT_TOL)
     eng.close()
+
+
+@pytest.mark.parametrize("rng", ["philox", "mt19937"])
+def test_replica_groups_on_streams_match_single_stream(rng):
+    """Splitting the batch over concurrent streams changes nothing bit-wise."""
+    L, T = 30, 60
+    reps = [_runner_params(r=2.0 + 0.25 * s, seed=s) for s in range(9)]
+    res = {}
+    for G in (1, 3, 4):
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=G)
+        assert eng.G == G
+        eng.run(snapshots=False)
+        res[G] = ([eng.final_state(k) for k in range(len(reps))], eng.stats.cpu().numpy(),
+                  eng.stop_iter.cpu().numpy())
+        eng.close()
+    for G in (3, 4):
+        for a, b in zip(res[1][0], res[G][0]):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y)
+        assert np.array_equal(res[1][2], res[G][2])
+        np.testing.assert_allclose(res[1][1], res[G][1], rtol=1e-12, atol=1e-12)

@@ -177,6 +177,11 @@ def main():
     step_agents = agent_steps / K
     achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
 
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "r01", "current", f"traffic_{args.config}.json")
+    if os.path.exists(tfile) and args.rng == "philox":
+        # measured HBM bytes per agent-step (rocprofv3 PMC passes of this same command)
+        traffic = json.load(open(tfile))["bytes_per_agent_step"] * step_agents
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world,
@@ -188,8 +193,12 @@ def main():
                        "rng": args.rng, "streams_per_gpu": eng.G,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "spgg_step_kernel (one launch per iteration)" if args.rng == "philox" else "spgg_mt_draw_kernel + spgg_step_kernel",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "bytes per iteration (all replicas), from profiles/r01/current/traffic_*.json",
+                         "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
+                         "kernel": (f"spgg_step_kernel, {eng.G} concurrent launches per iteration "
+                                    f"(one per replica group/stream)" if args.rng == "philox" else
+                                    "spgg_mt_draw_kernel + spgg_step_kernel per replica group"),
                          "device_ms_per_step": per_step_dev_s * 1e3},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -20,26 +20,71 @@ __device__ __forceinline__ int wrap(int x, int L) {
 
 // ---------------------------------------------------------------------------
 // Workgroup reduction of K per-thread f64 partials (K a power of two <= 64).
-// Butterfly "transpose" reduce: at each xor level a lane keeps one half of its
-// values and ships the other half, so K values cost ~K shuffles instead of
-// 6K.  Afterwards lane l holds the wave sum of value (l >> log2(64/K)).
+// Butterfly "transpose" reduce: at each level a lane keeps one half of its
+// values and receives the other half from a partner lane, so K values cost
+// ~K exchanges instead of 6K.  Afterwards lane l holds the wave sum of value
+// (l >> log2(64/K)).  Exchanges run on the VALU, never through the LDS pipe:
+//   bit 5 / bit 4: v_permlane32_swap / v_permlane16_swap (gfx950) swap the
+//                  kept and the shipped half in one instruction per dword
+//   bit 3 .. 0:    DPP row_ror:8, row_half_mirror, quad_perm — partners
+//                  l^8, l^7, l^2, l^1: each flips the level's bit and keeps
+//                  the higher bits, and together they span the 16-lane row.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// (a, b) -> (a', b') with a' + b' = the partner-summed kept value (MASK 32/16).
+template <int MASK>
+__device__ __forceinline__ double swap_sum(double a, double b) {
+  int alo = __double2loint(a), ahi = __double2hiint(a), blo = __double2loint(b), bhi = __double2hiint(b);
+  if constexpr (MASK == 32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+  }
+  return __hiloint2double(ahi, alo) + __hiloint2double(bhi, blo);
+}
+
+template <int MASK>
+__device__ __forceinline__ double partner(double x) {
+  if constexpr (MASK == 8) return dpp_f64<0x128>(x);   // row_ror:8      -> l^8
+  else if constexpr (MASK == 4) return dpp_f64<0x141>(x);  // row_half_mirror -> l^7
+  else if constexpr (MASK == 2) return dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
+  else return dpp_f64<0xB1>(x);                            // quad_perm [1,0,3,2]
+}
+
 template <int CNT, int MASK, int K>
 __device__ __forceinline__ void transpose_level(double (&v)[K], int lane) {
   if constexpr (MASK >= 1) {
-    if constexpr (CNT > 1) {
-      constexpr int h = CNT / 2;
-      const bool upper = (lane & MASK) != 0;
+    constexpr int h = CNT > 1 ? CNT / 2 : 1;
+    if constexpr (MASK >= 16) {
+      if constexpr (CNT > 1) {
 #pragma unroll
-      for (int i = 0; i < h; ++i) {
-        const double send = upper ? v[i] : v[i + h];
-        const double keep = upper ? v[i + h] : v[i];
-        v[i] = keep + __shfl_xor(send, MASK);
+        for (int i = 0; i < h; ++i) v[i] = swap_sum<MASK>(v[i], v[i + h]);
+      } else {
+        v[0] = swap_sum<MASK>(v[0], v[0]);
       }
-      transpose_level<h, MASK / 2, K>(v, lane);
     } else {
-      v[0] += __shfl_xor(v[0], MASK);
-      transpose_level<1, MASK / 2, K>(v, lane);
+      if constexpr (CNT > 1) {
+        const bool upper = (lane & MASK) != 0;
+#pragma unroll
+        for (int i = 0; i < h; ++i) {
+          const double send = upper ? v[i] : v[i + h];
+          const double keep = upper ? v[i + h] : v[i];
+          v[i] = keep + partner<MASK>(send);
+        }
+      } else {
+        v[0] += partner<MASK>(v[0]);
+      }
     }
+    transpose_level<(CNT > 1 ? CNT / 2 : 1), MASK / 2, K>(v, lane);
   }
 }
 

@@ -43,7 +43,8 @@
 using namespace spgg;
 
 // Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
-//   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute
+//   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
+//   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
@@ -190,15 +191,17 @@ __device__ __forceinline__ int wrap1(int x, int L, bool tiny) {
 // (J >= h*w/kBlock; host-checked).  Measured 5% faster than one-row-per-wave
 // staging (lane-constant columns but 28% idle lanes at 46-wide rows).
 template <int J, typename T>
-__device__ __forceinline__ void stage_region(T* dst, const T* src, int h, int w, int y0, int x0, int L,
-                                             bool tiny) {
+__device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, int h, int w, int y0, int x0,
+                                             int L, bool tiny) {
   const int total = h * w;
   const int tid = threadIdx.x;
   const int dr = kBlock / w, dc = kBlock - (kBlock / w) * w;
   int r = tid / w, c = tid - (tid / w) * w;
   T buf[J];
+  int di[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
+    di[j] = r * pitch + c;
     if (tid + j * kBlock < total) buf[j] = src[wrap1(y0 + r, L, tiny) * L + wrap1(x0 + c, L, tiny)];
     r += dr;
     c += dc;
@@ -209,7 +212,7 @@ __device__ __forceinline__ void stage_region(T* dst, const T* src, int h, int w,
   }
 #pragma unroll
   for (int j = 0; j < J; ++j)
-    if (tid + j * kBlock < total) dst[tid + j * kBlock] = buf[j];
+    if (tid + j * kBlock < total) dst[di[j]] = buf[j];
 }
 
 // 1/x to full f64 precision for DIAGNOSTIC quotients only (history values,
@@ -225,7 +228,9 @@ __device__ __forceinline__ double rcp_diag(double x) {
 enum { C_SWCD = 0, C_SWDC = 8, C_NCOOP1 = 16, C_NMD = 24 };   // cnt0
 enum { C_NMD2 = 0, C_GC0 = 8 };                                // cnt1: GC0..2 at 8,16,24; cnt2: GC3..5
 
-template <bool M2, bool AS, bool RQ, int RNG, int APT>
+// TWC > 0: compile-time tile width (LDS row pitches become immediates in every
+// stencil address); TWC = 0: run-time width.
+template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC>
 __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
   using RT = RStore<RQ>;
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
@@ -243,13 +248,17 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   const int tile = logical - rep * a.tiles_per_rep;
   const int st = a.stop_iter[rep];
   if (st != 0 && st < t) return;  // absorbed before t
+  if (SPGG_ABLATE & 64) return;
 
   const int L = a.L, n = a.n;
   const bool tiny = L < 8;
   const int tyi = tile / a.tiles_x, txi = tile - (tile / a.tiles_x) * a.tiles_x;
   const int y0 = tyi * a.TH, x0 = txi * a.TW;
   const int th = min(a.TH, L - y0), tw = min(a.TW, L - x0);
-  const LdsLayout ly = lds_layout(tw, th, HS, HR, HA, (int)sizeof(RT));
+  // LDS pitches from the full tile width (constants when TWC > 0); edge tiles
+  // use the top-left part of each region
+  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HR, HA, (int)sizeof(RT))
+                           : lds_layout(tw, th, HS, HR, HA, (int)sizeof(RT));
   double* tab = reinterpret_cast<double*>(smem);
   double* red = tab + 12;
   RT* sR = reinterpret_cast<RT*>(smem + ly.off_R);
@@ -317,8 +326,9 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     }
   }
   if (tid < 12) tab[tid] = tid < 6 ? pg.pay_c[tid] : pg.pay_d[tid - 6];
-  stage_region<(M2 ? 8 : 7)>(sS, a.S_in + rb, ly.sh, ly.sw, y0 - HS, x0 - HS, L, tiny);
-  if (!AS && !fin_only) stage_region<(M2 ? 8 : 6)>(sR, Rin + rb, ly.rh, ly.rw, y0 - HR, x0 - HR, L, tiny);
+  stage_region<(M2 ? 8 : 7)>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny);
+  if (!AS && !fin_only)
+    stage_region<(M2 ? 8 : 6)>(sR, ly.rw, Rin + rb, th + 2 * HR, tw + 2 * HR, y0 - HR, x0 - HR, L, tiny);
   __syncthreads();
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
@@ -344,7 +354,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         }
       }
     }
-    wave_partials<16>(v, red, 0);
+    if (!(SPGG_ABLATE & 8)) wave_partials<16>(v, red, 0);
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
@@ -417,17 +427,18 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
 
   // ---- phase 1c: recompute the ring of neighbours (distance <= M) --------
   if (acting && !(SPGG_ABLATE & 4)) {
-    const int band = HA * ly.aw;
-    const int ring = ly.aw * ly.ah - n_own;
+    const int aw = tw + 2 * HA;  // ring enumeration over the actual tile
+    const int band = HA * aw;
+    const int ring = aw * (th + 2 * HA) - n_own;
     for (int k = tid; k < ring; k += kBlock) {
       int ay, ax;
       if (k < band) {
-        ay = k / ly.aw;
-        ax = k - ay * ly.aw;
+        ay = k / aw;
+        ax = k - ay * aw;
       } else if (k < 2 * band) {
         const int k2 = k - band;
-        ay = HA + th + k2 / ly.aw;
-        ax = k2 - (k2 / ly.aw) * ly.aw;
+        ay = HA + th + k2 / aw;
+        ax = k2 - (k2 / aw) * aw;
       } else {
         const int k3 = k - 2 * band;
         ay = HA + k3 / (2 * HA);
@@ -553,12 +564,13 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     v[18] = (double)((cnt2 >> 16) & 0xff);
 #pragma unroll
     for (int k = 19; k < 32; ++k) v[k] = 0.0;
-    wave_partials<32>(v, red, 16);
+    if (!(SPGG_ABLATE & 8)) wave_partials<32>(v, red, 16);
   }
   __syncthreads();
 
   // ---- workgroup totals -> per-iteration history record ------------------
-  if (tid < 64) {
+  if ((SPGG_ABLATE & 8) && tid == 0 && tile == 0 && acting) srow[(size_t)(t + 1) * SPGG_NSTAT] = n / 2;
+  if (tid < 64 && !(SPGG_ABLATE & 8)) {
     double tot[2] = {0.0, 0.0};  // this slot and (for derived values) its "C" partner
     int slot = -1, k = -1, src = -1, src_c = -1;
     // Finalize group (slot t-1): sums over prev-D are total - prev-C.
@@ -795,7 +807,12 @@ template <bool M2, bool AS, bool RQ, int RNG>
 void launch_step_t(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
   const int total = c->cfg.n_rep * c->tiles_per_rep;
   const dim3 grid(((total + 7) / 8) * 8);
-  hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 4>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
+#ifndef SPGG_NO_TWC
+  if (c->TW == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 4, 40>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
+  else
+#endif
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 4, 0>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
 }
 
 template <bool M2, bool AS, bool RQ>

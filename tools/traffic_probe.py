@@ -41,6 +41,20 @@ def run(R, TW, TH, mode, L=200, K=100):
     del S, Rr, Q, md, atd
 
 
+import sys
+if "--copy" in sys.argv:  # plain device copy of the same Q bytes (read+write bandwidth reference)
+    for R in (105, 420):
+        a = torch.rand((R, 40000, 4), dtype=torch.float64, device=d)
+        b = torch.empty_like(a)
+        for _ in range(5):
+            b.copy_(a)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(100):
+            b.copy_(a)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) / 100 * 1e6
+        print(f"copy R={R}: {us:.1f} us  {2 * a.numel() * 8 / us / 1e6:.2f} TB/s", flush=True)
 for R in (26, 52, 105, 210, 420):
     run(R, 40, 25, 0)
     run(R, 40, 25, 2)

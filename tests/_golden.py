@@ -14,7 +14,7 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 _PARAM_KEYS = ("r", "c", "cost", "L", "iterations", "alpha", "gamma", "epsilon",
                "epsilon_decay", "epsilon_min", "influence_factor", "use_second_order",
                "lambda_epsilon", "delta_R_D", "R_min", "R_max",
-               "reward_weight_payoff", "rep_gain_C", "state_representation")
+               "reward_weight_payoff", "rep_gain_C", "state_representation", "algorithm")
 
 
 def case_names():
@@ -35,11 +35,19 @@ class Case:
         self.Sn = z["Sn"]
         self.ret = z["ret"]
         self.epsilon = float(z["epsilon"])
+        self.tables = (z["q_table_1"], z["q_table_2"]) if "q_table_1" in z.files else None
 
     @property
     def S_in_one(self):
         s = self.extra.get("S_in_one")
         return None if s is None else np.array(s)
+
+    @property
+    def algorithm(self):
+        from oracle.spgg_oracle import canonical_algorithm
+        alg = self.algorithm_instance
+        return canonical_algorithm(alg.get("kind", "qlearning") if alg else
+                                   self.kwargs.get("algorithm", "qlearning"))
 
     @property
     def algorithm_instance(self):
@@ -51,6 +59,7 @@ class Case:
         p = Params(**kw)
         alg = self.algorithm_instance
         if alg:
+            p.algorithm = alg.get("kind", "qlearning")
             p.alg_alpha, p.alg_gamma = alg["alpha"], alg["gamma"]
             p.epsilon, p.epsilon_decay, p.epsilon_min = (
                 alg["epsilon"], alg["epsilon_decay"], alg["epsilon_min"])

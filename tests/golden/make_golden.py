@@ -77,8 +77,38 @@ CASES = [
     for k in (1, 2, 3)
 ]
 
+# The other three operators of algorithms.py:136-341 (SARSA draws three times
+# per step, Double-Q keeps two tables and draws an extra rand per step).
+CASES += [
+    ("sarsa_m1_rep_L16", 20, dict(RUNNER, r=3.0, L=16, iterations=200, influence_factor=1.0,
+                                  use_second_order=False, reward_weight_payoff=0.95,
+                                  state_representation="reputation", algorithm="sarsa")),
+    ("sarsa_m2_act_L14", 21, dict(RUNNER, r=3.6, L=14, iterations=150, influence_factor=0.5,
+                                  use_second_order=True, reward_weight_payoff=1.0,
+                                  state_representation="action", algorithm="sarsa")),
+    ("esarsa_m1_rep_L16", 22, dict(RUNNER, r=3.0, L=16, iterations=200, influence_factor=1.0,
+                                   use_second_order=False, reward_weight_payoff=0.95,
+                                   state_representation="reputation", algorithm="expected_sarsa")),
+    ("esarsa_m2_rep_L18", 23, dict(RUNNER, r=4.2, L=18, iterations=150, influence_factor=1.5,
+                                   use_second_order=True, reward_weight_payoff=0.9,
+                                   state_representation="reputation", algorithm="expected-sarsa")),
+    ("dq_m1_rep_L16", 24, dict(RUNNER, r=3.0, L=16, iterations=200, influence_factor=1.0,
+                               use_second_order=False, reward_weight_payoff=0.95,
+                               state_representation="reputation", algorithm="double_qlearning")),
+    ("dq_m2_act_L15", 25, dict(RUNNER, r=3.8, L=15, iterations=150, influence_factor=1.0,
+                               use_second_order=True, reward_weight_payoff=1.0,
+                               state_representation="action", algorithm="double-q-learning")),
+    ("dq_m1_rep_L24_stopD", 26, dict(RUNNER, r=1.0, L=24, iterations=700, influence_factor=1.0,
+                                     use_second_order=False, reward_weight_payoff=0.95,
+                                     state_representation="reputation", algorithm="double_qlearning")),
+    ("sarsa_m2_rep_L20_stopC", 27, dict(RUNNER, r=5.0, L=20, iterations=800, influence_factor=1.0,
+                                        use_second_order=True, reward_weight_payoff=0.95,
+                                        state_representation="reputation", algorithm="sarsa")),
+]
+
 # Cases that need objects (S_in_one, an algorithm instance) are built below.
-SPECIAL = ["sinone_L16", "algo_instance_L16", "absorbing_init_L8"]
+SPECIAL = ["sinone_L16", "algo_instance_L16", "absorbing_init_L8",
+           "sarsa_instance_L16", "esarsa_instance_L16", "dq_instance_L16"]
 
 
 class _FakeH5File:
@@ -101,8 +131,9 @@ def _import_reference(ref):
     matplotlib.use("Agg")
     sys.modules["h5py"] = types.SimpleNamespace(File=_FakeH5File)
     sys.path.insert(0, ref)
-    from src.model import SPGG, QLearning  # noqa: E402
-    return SPGG, QLearning
+    from src.model import SPGG, QLearning, SARSA, ExpectedSARSA, DoubleQLearning  # noqa: E402
+    return SPGG, dict(qlearning=QLearning, sarsa=SARSA, expected_sarsa=ExpectedSARSA,
+                      double_qlearning=DoubleQLearning)
 
 
 def _pin_seed(seed):
@@ -134,19 +165,46 @@ def _save(name, seed, kwargs, m, ret, data, extra=None):
     out["Sn"] = np.asarray(m._Sn)
     out["ret"] = np.array([float(x) for x in ret])
     out["epsilon"] = np.array(m.algorithm.epsilon)
+    if getattr(m.algorithm, "q_table_1", None) is not None:   # Double-Q's two tables
+        out["q_table_1"] = m.algorithm.q_table_1
+        out["q_table_2"] = m.algorithm.q_table_2
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated name prefixes to (re)generate")
     args = ap.parse_args()
-    SPGG, QLearning = _import_reference(args.ref)
+    SPGG, ALGS = _import_reference(args.ref)
+    QLearning = ALGS["qlearning"]
+    only = [x for x in args.only.split(",") if x]
+
+    def want(name):
+        return not only or any(name.startswith(o) for o in only)
+
     with tempfile.TemporaryDirectory() as tmp:
         for name, seed, kw in CASES:
+            if not want(name):
+                continue
             m, ret, data = _run(SPGG, seed, kw, tmp)
             _save(name, seed, kw, m, ret, data)
             print(name, "iters", len(data["coop_rate_history"]), "coop", ret[0])
+
+        # algorithm instances of the other operators, with their own hyper-parameters
+        for name, seed, kind, m2, state in (("sarsa_instance_L16", 30, "sarsa", True, "reputation"),
+                                            ("esarsa_instance_L16", 31, "expected_sarsa", False, "action"),
+                                            ("dq_instance_L16", 32, "double_qlearning", True, "reputation")):
+            if not want(name):
+                continue
+            alg = dict(alpha=0.6, gamma=0.85, epsilon=0.4, epsilon_decay=0.97, epsilon_min=0.02)
+            kw = dict(RUNNER, r=3.4, L=16, iterations=120, influence_factor=1.0,
+                      use_second_order=m2, reward_weight_payoff=0.95, state_representation=state)
+            m, ret, data = _run(SPGG, seed, dict(kw, algorithm=ALGS[kind](**alg)), tmp)
+            _save(name, seed, kw, m, ret, data, extra={"algorithm_instance": dict(alg, kind=kind)})
+            print(name, "iters", len(data["coop_rate_history"]), "coop", ret[0])
+        if only and not any(want(n) for n in ("sinone_L16", "algo_instance_L16", "absorbing_init_L8")):
+            return
 
         # S_in_one supplied: no population draw (spgg.py:161-162)
         rs = np.random.RandomState(99)

@@ -38,8 +38,8 @@ def record_from_oracle(c):
         if nc == 0 or nc == n:
             stopped = True
             break
-        u, b = O.draw_step(rs, L)
-        S, R, Q, d = O.step(S, R, Q, eps, u, b, p, P=P)
+        draws = O.draw_step(rs, L)
+        S, R, Q, d = O.step(S, R, Q, eps, draws, p=p, P=P)
         eps = max(eps * p.epsilon_decay, p.epsilon_min)
         a, ps = d["_actions"], d["_prev_S"]
         rew, rr = d["_rewards"], d["_rep_reward"]

@@ -18,3 +18,6 @@ def test_oracle_matches_reference_bit_exact(name):
     assert np.array_equal(fin["S"], c.Sn)
     assert np.array_equal(np.array(fin["ret"], dtype=float), c.ret)
     assert fin["epsilon"] == c.epsilon
+    if c.tables is not None:  # Double-Q's own tables (algorithm.q_table_1/2)
+        assert np.array_equal(fin["tables"][0], c.tables[0])
+        assert np.array_equal(fin["tables"][1], c.tables[1])

@@ -21,7 +21,7 @@ def record_from_oracle(c):
     T = p.iterations
     st = np.zeros((T + 2, C.NSTAT))
     rs = np.random.RandomState(c.seed)
-    Q = rs.uniform(low=-0.01, high=0.01, size=(L, L, 2, 2))
+    Q, tables = O.init_tables(p, rs)
     S = rs.randint(0, 2, size=(L, L)) if c.S_in_one is None else c.S_in_one
     R = np.zeros((L, L))
     eps = p.epsilon
@@ -38,8 +38,8 @@ def record_from_oracle(c):
         if nc == 0 or nc == n:
             stopped = True
             break
-        draws = O.draw_step(rs, L)
-        S, R, Q, d = O.step(S, R, Q, eps, draws, p=p, P=P)
+        draws = O.draw_step(rs, L, p.algorithm)
+        S, R, Q, d = O.step(S, R, Q, eps, draws, p=p, P=P, tables=tables)
         eps = max(eps * p.epsilon_decay, p.epsilon_min)
         a, ps = d["_actions"], d["_prev_S"]
         rew, rr = d["_rewards"], d["_rep_reward"]

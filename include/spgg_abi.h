@@ -5,10 +5,12 @@
  * Replaces, per executed iteration of the reference's run loop:
  *   - payoff of the 5 overlapping groups      src/model/spgg.py:23-36, 230-279, 373-378
  *   - state representation (reputation/action) src/model/spgg.py:281-317, 409, 423
- *   - eps-greedy action select                 src/model/algorithms.py:102-110
+ *   - eps-greedy action select                 src/model/algorithms.py:102-110 (+ copies)
  *   - reputation update                        src/model/spgg.py:319-323, 413-416
  *   - reward                                   src/model/spgg.py:424-427
- *   - Q-learning TD update                     src/model/algorithms.py:112-133
+ *   - TD update of the RL operator             src/model/algorithms.py:112-341
+ *       Q-learning :112-133, SARSA :152-178 (+ spgg.py:432-438), Expected SARSA
+ *       :191-234, Double Q-learning :285-341 (+ spgg.py:496-505)
  *   - diagnostic TD + neighbor-influence term  src/model/spgg.py:445-509
  *   - per-step history reductions              src/model/spgg.py:380-394, 418-420, 511-545, 561-592
  * The reference has no native layer; this ABI is what its Python would bind
@@ -32,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 5
+#define SPGG_ABI_VERSION 6
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -43,8 +45,14 @@ extern "C" {
 #define SPGG_STATE_REPUTATION 0
 #define SPGG_STATE_ACTION 1
 
-/* random stream used by the eps-greedy select */
-#define SPGG_RNG_INJECT 0   /* caller fills explore/bit bytes per step (host MT19937 etc.) */
+/* RL operator (algorithms.py:344-383) */
+#define SPGG_ALG_QLEARNING 0
+#define SPGG_ALG_SARSA 1
+#define SPGG_ALG_EXPECTED_SARSA 2
+#define SPGG_ALG_DOUBLE_Q 3
+
+/* random stream used by the eps-greedy selects */
+#define SPGG_RNG_INJECT 0   /* caller fills the draw planes per step (host MT19937 etc.) */
 #define SPGG_RNG_MT19937 1  /* device MT19937, bit-identical to numpy.random.RandomState */
 #define SPGG_RNG_PHILOX 2   /* counter-based Philox4x32-10 keyed by (seed, replica, step, agent) */
 
@@ -86,6 +94,7 @@ typedef struct {
   int32_t iterations;    /* capacity: stats/eps tables hold iterations+2 slots */
   int32_t rep_int8;      /* 1: R buffers hold int8 multiples of each replica's rep_unit
                             (exact when gains/bounds are dyadic multiples, see below) */
+  int32_t algorithm;     /* SPGG_ALG_* */
 } spgg_config;
 
 /* Per-replica constants, precomputed by the host in the reference's own
@@ -132,11 +141,19 @@ typedef struct {
  *   R[2]      f64    [n_rep][n]      reputation R_t (int8 R_t/rep_unit if rep_int8)
  *   Q[2]      f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2);
  *                                    Q[(t-1)&1] holds iteration t-1's TD update
- *                                    without its NI term (applied by iteration t)
+ *                                    without its NI term (applied by iteration t).
+ *                                    Double Q-learning: [n_rep][n][2][2][2] =
+ *                                    q_table_1[s][a] then q_table_2[s][a] per agent
  *   md[2]     f64    [n_rep][n]      max(0, max_diff) of iteration t-1
  *   atd       f32    [n_rep][n]      |alpha*td'| of the pending iteration (diagnostic)
- *   explore   uint8  [n_rep][n]      eps-greedy explore flag of the step (INJECT/MT19937)
- *   rbit      uint8  [n_rep][n]      random action of the step          (INJECT/MT19937)
+ *   draws     uint8  [planes][..][n] the step's random draws as 0/1 bytes (INJECT/MT19937),
+ *                                    one plane per draw of the reference, in its order
+ *                                    (spgg_draw_planes): plane 2k = (rand < eps) and
+ *                                    2k+1 = randint(0,2) of select k (k = 0 the action;
+ *                                    SARSA k = 1 next action, k = 2 diagnostic, spgg.py:
+ *                                    434,452); Double-Q plane 2 = (rand < 0.5), the table
+ *                                    choice (algorithms.py:302).  Replica rep of plane p
+ *                                    is at draws + p*draw_plane_stride + rep*n
  *   mt_state  uint32 [n_rep][625]    MT19937 key[624] + pos (MT19937 only)
  *   eps       f64    [n_rep][iterations+2]  eps used by iteration t
  *   stats     f64    [n_rep][iterations+2][SPGG_NSTAT]  zero-initialised; slot
@@ -153,8 +170,8 @@ typedef struct {
   double* Q[2];
   double* md[2];
   float* atd;
-  uint8_t* explore;
-  uint8_t* rbit;
+  uint8_t* draws;
+  int64_t draw_plane_stride;  /* bytes between draw planes (>= n_rep*n) */
   uint32_t* mt_state;
   double* eps;
   double* stats;
@@ -162,6 +179,8 @@ typedef struct {
 } spgg_buffers;
 
 int spgg_abi_version(void);
+/* Number of draw planes one iteration of `algorithm` consumes: 2, 6 (SARSA), 2, 3 (Double-Q). */
+int spgg_draw_planes(int32_t algorithm);
 const char* spgg_last_error(const spgg_ctx* ctx);
 
 int spgg_create(spgg_ctx** out, const spgg_config* cfg);
@@ -172,7 +191,7 @@ int spgg_bind(spgg_ctx* ctx, const spgg_buffers* bufs);
 /* Enqueue iterations t0 .. t0+n_steps-1 (1-based, as the reference's loop
  * variable i, spgg.py:368).  Replicas that reach an absorbing state stop by
  * themselves (spgg.py:405-406).  In SPGG_RNG_INJECT mode n_steps must be 1
- * and the explore/rbit bytes of iteration t0 must already be in place. */
+ * and the draw planes of iteration t0 must already be in place. */
 int spgg_step(spgg_ctx* ctx, int32_t t0, int32_t n_steps, void* hip_stream);
 
 /* Apply the deferred neighbor-influence term of iteration t_last (the last

@@ -13,11 +13,15 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
 RNG_MODES = {"inject": RNG_INJECT, "mt19937": RNG_MT19937, "philox": RNG_PHILOX}
+ALG_QLEARNING, ALG_SARSA, ALG_EXPECTED_SARSA, ALG_DOUBLE_Q = 0, 1, 2, 3
+ALGORITHMS = {"qlearning": ALG_QLEARNING, "sarsa": ALG_SARSA, "expected_sarsa": ALG_EXPECTED_SARSA,
+              "double_qlearning": ALG_DOUBLE_Q}
+DRAW_PLANES = {ALG_QLEARNING: 2, ALG_SARSA: 6, ALG_EXPECTED_SARSA: 2, ALG_DOUBLE_Q: 3}
 
 # stats record layout (enum in spgg_abi.h)
 ST_NCOOP, ST_SUMP, ST_SUMP_C, ST_SUMP_D, ST_SUMR = 0, 1, 2, 3, 4
@@ -29,14 +33,14 @@ NSTAT = 34
 
 EXPORTED = ("spgg_abi_version", "spgg_last_error", "spgg_create", "spgg_set_params",
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
-            "spgg_destroy")
+            "spgg_destroy", "spgg_draw_planes")
 
 
 class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("n_rep", ctypes.c_int32), ("L", ctypes.c_int32),
                 ("second_order", ctypes.c_int32), ("state_mode", ctypes.c_int32),
                 ("rng_mode", ctypes.c_int32), ("iterations", ctypes.c_int32),
-                ("rep_int8", ctypes.c_int32)]
+                ("rep_int8", ctypes.c_int32), ("algorithm", ctypes.c_int32)]
 
 
 class RepParams(ctypes.Structure):
@@ -52,8 +56,8 @@ class RepParams(ctypes.Structure):
 
 class Buffers(ctypes.Structure):
     _fields_ = [("S", ctypes.c_void_p * 2), ("R", ctypes.c_void_p * 2), ("Q", ctypes.c_void_p * 2),
-                ("md", ctypes.c_void_p * 2), ("atd", ctypes.c_void_p), ("explore", ctypes.c_void_p),
-                ("rbit", ctypes.c_void_p), ("mt_state", ctypes.c_void_p), ("eps", ctypes.c_void_p),
+                ("md", ctypes.c_void_p * 2), ("atd", ctypes.c_void_p), ("draws", ctypes.c_void_p),
+                ("draw_plane_stride", ctypes.c_int64), ("mt_state", ctypes.c_void_p), ("eps", ctypes.c_void_p),
                 ("stats", ctypes.c_void_p), ("stop_iter", ctypes.c_void_p)]
 
 
@@ -100,6 +104,8 @@ def load(path: str | None = None):
         lib.spgg_tile_shape.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         lib.spgg_destroy.restype = ctypes.c_int
         lib.spgg_destroy.argtypes = [vp]
+        lib.spgg_draw_planes.restype = ctypes.c_int
+        lib.spgg_draw_planes.argtypes = [i32]
         v = lib.spgg_abi_version()
         if v != ABI_VERSION:
             raise SpggError(f"libspgg_hip ABI {v} != expected {ABI_VERSION}")

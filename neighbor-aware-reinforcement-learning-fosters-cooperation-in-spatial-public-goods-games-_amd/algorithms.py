@@ -7,9 +7,9 @@ factory with its ValueError.  Their per-lattice `select_action` /
 driven by `SPGG.run` / `BatchEngine`; calling those two methods on their own
 raises, because this package has no NumPy execution path by design.
 
-GPU coverage: QLearning (algorithms.py:96-133).  SARSA, ExpectedSARSA and
-DoubleQLearning are accepted by the factory (same names, same errors) but
-`SPGG.run` raises NotImplementedError for them until their kernels land.
+GPU coverage: all four operators -- QLearning (algorithms.py:96-133), SARSA
+(:136-178), ExpectedSARSA (:181-234), DoubleQLearning (:237-341) -- each a
+template instance of the step kernel (spgg_kernels.hip, SPGG_ALG_*).
 """
 from __future__ import annotations
 
@@ -81,6 +81,23 @@ class DoubleQLearning(RLAlgorithm):
         if self.q_table_1 is None or self.q_table_2 is None:
             raise ValueError("Q-tables not initialized. Call initialize_q_tables first.")
         return (self.q_table_1 + self.q_table_2) / 2
+
+
+_ALIASES = {"qlearning": "qlearning", "q-learning": "qlearning", "sarsa": "sarsa",
+            "expected_sarsa": "expected_sarsa", "expected-sarsa": "expected_sarsa",
+            "double_qlearning": "double_qlearning", "double-q-learning": "double_qlearning"}
+
+
+def canonical_name(algorithm) -> str:
+    """Operator kind of a name (create_algorithm's accepted spellings, algorithms.py:371-383)
+    or of an RLAlgorithm instance."""
+    if isinstance(algorithm, RLAlgorithm):
+        return algorithm.kind
+    name = str(algorithm).lower()
+    if name not in _ALIASES:
+        raise ValueError(f"Unknown algorithm: {name}. "
+                         f"Supported: 'qlearning', 'sarsa', 'expected_sarsa', 'double_qlearning'")
+    return _ALIASES[name]
 
 
 def create_algorithm(algorithm_name: str, alpha: float, gamma: float,

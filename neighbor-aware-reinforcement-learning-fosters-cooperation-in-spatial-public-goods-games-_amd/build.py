@@ -7,6 +7,8 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
@@ -14,7 +16,11 @@ SRC = [os.path.join(PKG_DIR, "csrc", "spgg_kernels.hip")]
 INC = os.path.join(ROOT, "include")
 OUT = os.path.join(PKG_DIR, "libspgg_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+# One translation unit per RL operator (its step kernels) + one for the C ABI,
+# compiled in parallel and linked into one shared library (spgg_kernels.hip's
+# SPGG_TU switch).
+TUS = (0, 1, 2, 3, 9)
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # bit-exact f64: no FMA contraction of the reference's a*b+c
          "-ffp-contract=off",
          # f64 global atomics as hardware global_atomic_add_f64 (no CAS loop)
@@ -29,14 +35,25 @@ def needs_build(out=OUT):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
-        return OUT
-    cmd = [HIPCC, *FLAGS, f"-I{INC}", "-o", OUT, *SRC]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    return OUT
+def build(force=False, verbose=True, out=OUT, defines=()):
+    if not force and not needs_build(out):
+        return out
+    extra = [f"-D{d}" for d in defines]
+    with tempfile.TemporaryDirectory() as tmp:
+        objs = [os.path.join(tmp, f"tu{k}.o") for k in TUS]
+        cmds = [[HIPCC, *FLAGS, *extra, f"-DSPGG_TU={k}", f"-I{INC}", "-c", SRC[0], "-o", o]
+                for k, o in zip(TUS, objs)]
+        if verbose:
+            print(" ".join(cmds[0]).replace("-DSPGG_TU=0", "-DSPGG_TU={0,1,2,3,9}"), flush=True)
+        jobs = max(1, min(len(cmds), os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "8"))))
+        with ThreadPoolExecutor(jobs) as ex:
+            for r in ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds):
+                if r.returncode:
+                    sys.stderr.write(r.stdout + r.stderr)
+                    raise subprocess.CalledProcessError(r.returncode, r.args)
+        link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs]
+        subprocess.run(link, check=True)
+    return out
 
 
 if __name__ == "__main__":

@@ -49,9 +49,17 @@ using namespace spgg;
 #define SPGG_ABLATE 0
 #endif
 
-namespace {
+// Build layout: this file is compiled once per RL operator with
+// -DSPGG_TU=<SPGG_ALG_*> (that operator's step kernels only) and once with
+// -DSPGG_TU=9 (C ABI, MT19937 and payoff kernels); without SPGG_TU it is one
+// translation unit with everything.  The pieces meet in spgg_impl.
+#ifndef SPGG_TU
+#define SPGG_TU (-1)
+#endif
+#define SPGG_TU_HAS_ALG(k) (SPGG_TU == -1 || SPGG_TU == (k))
+#define SPGG_TU_HAS_HOST (SPGG_TU == -1 || SPGG_TU == 9)
 
-constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
+namespace spgg_impl {
 
 struct TileArgs {
   const uint8_t* S_in;  // S_t   (bit0 strategy, bits1-3 pending-NI bookkeeping)
@@ -63,14 +71,36 @@ struct TileArgs {
   const double* md_in;  // max(0, max_diff) of t-1
   double* md_out;
   float* atd;           // |alpha*td'| of the pending iteration (owner only)
-  const uint8_t* explore;
-  const uint8_t* rbit;
+  const uint8_t* draws;  // draw planes (INJECT / MT19937), plane stride `plane`
+  size_t plane;
   const double* eps;
   double* stats;
   int* stop_iter;
   const spgg_rep_params* params;
   int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
 };
+
+// What a step launch needs to pick and size the kernel instance.
+struct LaunchCfg {
+  int m2, as, rq, rng, tw, total_tiles;
+  size_t lds_bytes;
+};
+
+// Enqueue one step-kernel launch of operator ALG (defined in that operator's TU).
+template <int ALG>
+void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s);
+
+// Agents per thread of operator ALG's kernel (Double-Q holds two tables in registers).
+constexpr int apt_of(int alg) { return alg == SPGG_ALG_DOUBLE_Q ? 2 : 4; }
+
+}  // namespace spgg_impl
+
+using spgg_impl::TileArgs;
+
+namespace {
+
+constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
+
 
 struct LdsLayout {
   int sw, sh, rw, rh, aw, ah;
@@ -228,14 +258,168 @@ __device__ __forceinline__ double rcp_diag(double x) {
 enum { C_SWCD = 0, C_SWDC = 8, C_NCOOP1 = 16, C_NMD = 24 };   // cnt0
 enum { C_NMD2 = 0, C_GC0 = 8 };                                // cnt1: GC0..2 at 8,16,24; cnt2: GC3..5
 
+// Q table helpers.  QB = 1 for Double Q-learning (second table qb), else the
+// qb arrays are dead and the compiler drops them.
+enum { ALG_Q = SPGG_ALG_QLEARNING, ALG_SARSA = SPGG_ALG_SARSA, ALG_ES = SPGG_ALG_EXPECTED_SARSA,
+       ALG_DQ = SPGG_ALG_DOUBLE_Q };
+
+// argmax over the two actions of a Q row, ties -> action 0 (np.argmax, algorithms.py:106-107)
+__device__ __forceinline__ int greedy2(double v0, double v1) { return v0 >= v1 ? 0 : 1; }
+
+// Double-Q's combined table entry (q1 + q2) / 2 (algorithms.py:262-266); the
+// halving is exact, so * 0.5 is the same double.
+__device__ __forceinline__ double mean2(double x, double y) { return (x + y) * 0.5; }
+
+// E[Q(s', .)] under the eps-greedy policy: probabilities eps/2 and
+// (1 - eps) + eps/2 on the greedy action, summed p0*q0 + p1*q1
+// (algorithms.py:205-222, spgg.py:455-462).
+__device__ __forceinline__ double expected_q(double v0, double v1, double eps) {
+  const double po = eps * 0.5;            // eps / num_actions
+  const double pgr = (1.0 - eps) + po;    // (1 - eps) + eps / num_actions
+  const int g = greedy2(v0, v1);
+  return (g == 0 ? pgr : po) * v0 + (g == 1 ? pgr : po) * v1;
+}
+
+// Draw pair k of agent g at iteration t: explore flag (rand < thr) and the
+// randint bit.  Philox: counter (agent, t + k*2^26) under the replica key;
+// device MT19937 / inject: planes 2k, 2k+1 of the draw record.
+template <int RNG>
+__device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, int t, uint32_t key, double thr,
+                                          int k, int* ex, int* rbt) {
+  if constexpr (RNG == SPGG_RNG_PHILOX) {
+#if SPGG_ABLATE & 1
+    *ex = ((g * 2654435761u + t + k) >> 7) % 50 == 0; *rbt = (g ^ t ^ k) & 1;
+#else
+    philox_draw(g, t + (k << 26), key, thr, ex, rbt);
+#endif
+  } else {
+    *ex = a.draws[(size_t)(2 * k) * a.plane + rb + g];
+    *rbt = a.draws[(size_t)(2 * k + 1) * a.plane + rb + g];
+  }
+}
+
+// Double-Q's table choice (rand < 0.5, algorithms.py:302): plane 2, or Philox pair 1.
+template <int RNG>
+__device__ __forceinline__ int draw_table1(const TileArgs& a, size_t rb, int g, int t, uint32_t key) {
+  if constexpr (RNG == SPGG_RNG_PHILOX) {
+    int ex, rbt;
+    philox_draw(g, t + (1 << 26), key, 0.5, &ex, &rbt);
+    return ex;
+  } else {
+    return a.draws[(size_t)2 * a.plane + rb + g];
+  }
+}
+
+template <int QB>
+__device__ __forceinline__ void load_q(const double* Q, size_t agent, double (&q)[4], double (&qb)[QB ? 4 : 1]) {
+  const double2* qp = reinterpret_cast<const double2*>(Q + agent * (QB ? 8 : 4));
+  const double2 q01 = qp[0], q23 = qp[1];
+  q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
+  if constexpr (QB) {
+    const double2 b01 = qp[2], b23 = qp[3];
+    qb[0] = b01.x; qb[1] = b01.y; qb[2] = b23.x; qb[3] = b23.y;
+  }
+}
+
+template <int QB>
+__device__ __forceinline__ void store_q(double* Q, size_t agent, const double (&q)[4],
+                                        const double (&qb)[QB ? 4 : 1]) {
+  double2* qo = reinterpret_cast<double2*>(Q + agent * (QB ? 8 : 4));
+  qo[0] = make_double2(q[0], q[1]);
+  qo[1] = make_double2(q[2], q[3]);
+  if constexpr (QB) {
+    qo[2] = make_double2(qb[0], qb[1]);
+    qo[3] = make_double2(qb[2], qb[3]);
+  }
+}
+
+// Q row of state s the eps-greedy select reads (Double-Q: the mean table).
+template <int QB>
+__device__ __forceinline__ void select_row(const double (&q)[4], const double (&qb)[QB ? 4 : 1], int s,
+                                           double* v0, double* v1) {
+  if constexpr (QB) {
+    const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
+    const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
+    *v0 = s ? m10 : m00;
+    *v1 = s ? m11 : m01;
+  } else {
+    *v0 = s ? q[2] : q[0];
+    *v1 = s ? q[3] : q[1];
+  }
+}
+
+// TD update of the operator for one agent (algorithms.py:112-341) and the
+// diagnostic TD on the updated table (spgg.py:446-473).  Returns |diag_alpha*td'|.
+template <int ALG, int RNG>
+__device__ __forceinline__ float td_update(const TileArgs& a, const spgg_rep_params& pg, size_t rb, int g, int t,
+                                           uint32_t key, double eps, double rew, int so, int act, int sn,
+                                           double (&q)[4], double (&qb)[ALG == ALG_DQ ? 4 : 1]) {
+  const double alpha = pg.alpha, gamma = pg.gamma, dgamma = pg.diag_gamma;
+  const int e = so * 2 + act;
+  double td2;
+  if constexpr (ALG == ALG_DQ) {
+    // scalar copies: value selects only (pointer selects into the tables
+    // would keep them out of registers)
+    double x[4] = {q[0], q[1], q[2], q[3]}, y[4] = {qb[0], qb[1], qb[2], qb[3]};
+    const int up1 = draw_table1<RNG>(a, rb, g, t, key);
+    const double qc1 = q_get(x, e), qc2 = q_get(y, e);
+    const double y0 = y[0], y1 = y[1], y2 = y[2], y3 = y[3];
+    const double x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
+    const double b0 = sn ? y2 : y0, b1 = sn ? y3 : y1;  // q_table_2[s']
+    const double c0 = sn ? x2 : x0, c1 = sn ? x3 : x1;  // q_table_1[s']
+    const double n1 = b0 >= b1 ? b0 : b1;  // q2 at its argmax (algorithms.py:317-323)
+    const double n2 = c0 >= c1 ? c0 : c1;
+    const double u1 = qc1 + alpha * ((rew + gamma * n1) - qc1);
+    const double u2 = qc2 + alpha * ((rew + gamma * n2) - qc2);
+    const double nq1 = up1 ? u1 : qc1, nq2 = up1 ? qc2 : u2;
+    q[0] = e == 0 ? nq1 : x0; q[1] = e == 1 ? nq1 : x1; q[2] = e == 2 ? nq1 : x2; q[3] = e == 3 ? nq1 : x3;
+    qb[0] = e == 0 ? nq2 : y0; qb[1] = e == 1 ? nq2 : y1; qb[2] = e == 2 ? nq2 : y2; qb[3] = e == 3 ? nq2 : y3;
+    // diagnostic on the mean table (spgg.py:463-467)
+    const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
+    const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
+    const double m0 = sn ? m10 : m00, m1 = sn ? m11 : m01;
+    td2 = (rew + dgamma * fmax(m0, m1)) - mean2(nq1, nq2);
+  } else {
+    const double qc = q_get(q, e);
+    const double v0 = sn ? q[2] : q[0], v1 = sn ? q[3] : q[1];
+    double target;
+    if constexpr (ALG == ALG_Q) {
+      target = fmax(v0, v1);                                         // algorithms.py:124-127
+    } else if constexpr (ALG == ALG_SARSA) {
+      int ex, rbt;                                                   // next action, spgg.py:434
+      draw_pair<RNG>(a, rb, g, t, key, eps, 1, &ex, &rbt);
+      target = (ex ? rbt : greedy2(v0, v1)) ? v1 : v0;               // algorithms.py:168-171
+    } else {
+      target = expected_q(v0, v1, eps);                              // algorithms.py:205-222
+    }
+    const double td = (rew + gamma * target) - qc;
+    const double q1 = qc + alpha * td;
+    q_set(q, e, q1);
+    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];       // updated table
+    double target2;
+    if constexpr (ALG == ALG_SARSA) {
+      int ex, rbt;                                                   // diagnostic select, spgg.py:452
+      draw_pair<RNG>(a, rb, g, t, key, eps, 2, &ex, &rbt);
+      target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
+    } else if constexpr (ALG == ALG_ES) {
+      target2 = expected_q(w0, w1, eps);
+    } else {
+      target2 = fmax(w0, w1);
+    }
+    td2 = (rew + dgamma * target2) - q1;
+  }
+  return (float)fabs(pg.diag_alpha * td2);
+}
+
 // TWC > 0: compile-time tile width (LDS row pitches become immediates in every
 // stencil address); TWC = 0: run-time width.
-template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC>
+template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
 __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
   using RT = RStore<RQ>;
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
   constexpr int HR = 2 * HA;      // R_t halo: states of ring agents
   constexpr int HS = HA + 2;      // S_t halo: payoffs of ring agents
+  constexpr int QB = ALG == ALG_DQ ? 1 : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -293,6 +477,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
   int gidx[APT], rc[APT];
   double q[APT][4];
+  double qb[APT][QB ? 4 : 1];
   double md_own[APT];
   float atd_own[APT];
   const int n_own = th * tw;
@@ -307,11 +492,10 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       md_own[u] = 0.0;
       atd_own[u] = 0.f;
       q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
+      if constexpr (QB) qb[u][0] = qb[u][1] = qb[u][2] = qb[u][3] = 0.0;
       if (k < n_own) {
         gidx[u] = (y0 + r) * L + (x0 + c);
-        const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + gidx[u]) * 4);
-        const double2 q01 = qp[0], q23 = qp[1];
-        q[u][0] = q01.x; q[u][1] = q01.y; q[u][2] = q23.x; q[u][3] = q23.y;
+        load_q<QB>(a.Q_in, rb + gidx[u], q[u], qb[u]);
         if (pending) {
           md_own[u] = a.md_in[rb + gidx[u]];
           atd_own[u] = a.atd[rb + gidx[u]];
@@ -344,25 +528,28 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
         const double nu = apply_pending(q[u], b, md_own[u], kappa, lam_den, lam_rcp);
+        if constexpr (QB) {  // both tables (spgg.py:496-502)
+          const int e = ((b >> 1) & 1) * 2 + (b & 1);
+          q_set(qb[u], e, q_get(qb[u], e) + nu);
+        }
         const double anu = fabs(nu);
         v[0] += (anu * rcp_diag(((double)atd_own[u] + anu) + 1e-8)) * 100.0;  // spgg.py:512
         const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                        // prev_S of t-1 == C
 #pragma unroll
         for (int e = 0; e < 4; ++e) {                                          // spgg.py:562-583
-          v[1 + e] += q[u][e];
-          v[5 + e] += q[u][e] * cm;
+          const double qv = QB ? mean2(q[u][e], qb[u][QB ? e : 0]) : q[u][e];
+          v[1 + e] += qv;
+          v[5 + e] += qv * cm;
         }
       }
     }
-    if (!(SPGG_ABLATE & 8)) wave_partials<16>(v, red, 0);
+    wave_partials<16>(v, red, 0);
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       if (gidx[u] < 0) continue;
-      double2* qo = reinterpret_cast<double2*>(a.Q_out + (rb + gidx[u]) * 4);
-      qo[0] = make_double2(q[u][0], q[u][1]);
-      qo[1] = make_double2(q[u][2], q[u][3]);
+      store_q<QB>(a.Q_out, rb + gidx[u], q[u], qb[u]);
     }
   }
 
@@ -392,18 +579,10 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     if constexpr (AS) so = s_t == 0 ? 1 : 0;
     else so = rep_state_lds<M2>(sR, (r + HR) * ly.rw + (c + HR), ly.rw);
     int ex, rbt;                                          // algorithms.py:105-109
-    if constexpr (RNG == SPGG_RNG_PHILOX) {
-#if SPGG_ABLATE & 1
-      ex = ((gidx[u] * 2654435761u + t) >> 7) % 50 == 0; rbt = (gidx[u] ^ t) & 1;
-#else
-      philox_draw(gidx[u], t, pkey, eps_t, &ex, &rbt);
-#endif
-    } else {
-      ex = a.explore[rb + gidx[u]];
-      rbt = a.rbit[rb + gidx[u]];
-    }
-    const double qs0 = so ? q[u][2] : q[u][0], qs1 = so ? q[u][3] : q[u][1];
-    const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);    // argmax ties -> 0
+    draw_pair<RNG>(a, rb, gidx[u], t, pkey, eps_t, 0, &ex, &rbt);
+    double qs0, qs1;
+    select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
+    const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0
     const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
     const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
     const double wpp = w_p * P, wrr = w_rep * rr;
@@ -449,10 +628,15 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
       const uint8_t b = sS[cs];
       const int s_t = b & 1;
-      const double2* qp = reinterpret_cast<const double2*>(a.Q_in + (rb + g) * 4);
-      const double2 q01 = qp[0], q23 = qp[1];
-      double qq[4] = {q01.x, q01.y, q23.x, q23.y};
-      if (pending) apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den, lam_rcp);
+      double qq[4], qqb[QB ? 4 : 1];
+      load_q<QB>(a.Q_in, rb + g, qq, qqb);
+      if (pending) {
+        const double nu = apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den, lam_rcp);
+        if constexpr (QB) {
+          const int e = ((b >> 1) & 1) * 2 + (b & 1);
+          q_set(qqb, e, q_get(qqb, e) + nu);
+        }
+      }
       const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
       int so;
       RVal<RQ> r_t;
@@ -465,18 +649,10 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         r_t = sR[cr];
       }
       int ex, rbt;
-      if constexpr (RNG == SPGG_RNG_PHILOX) {
-#if SPGG_ABLATE & 1
-        ex = ((g * 2654435761u + t) >> 7) % 50 == 0; rbt = (g ^ t) & 1;
-#else
-        philox_draw(g, t, pkey, eps_t, &ex, &rbt);
-#endif
-      } else {
-        ex = a.explore[rb + g];
-        rbt = a.rbit[rb + g];
-      }
-      const double qs0 = so ? qq[2] : qq[0], qs1 = so ? qq[3] : qq[1];
-      const int act = ex ? rbt : ((qs0 >= qs1) ? 0 : 1);
+      draw_pair<RNG>(a, rb, g, t, pkey, eps_t, 0, &ex, &rbt);
+      double qs0, qs1;
+      select_row<QB>(qq, qqb, so, &qs0, &qs1);
+      const int act = ex ? rbt : greedy2(qs0, qs1);
       const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
       const double rew = w_p * P + w_rep * (act == 0 ? 0.5 : 0.0);
       const int ca = ay * ly.aw + ax;
@@ -490,7 +666,6 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;
   if (acting) {
-    const double alpha = pg.alpha, gamma = pg.gamma, dalpha = pg.diag_alpha, dgamma = pg.diag_gamma;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       if (gidx[u] < 0) continue;
@@ -501,20 +676,8 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      // Q-learning TD, algorithms.py:121-131
-      const int e = so * 2 + act;
-      const double qc = q_get(q[u], e);
-      const double m = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
-      const double td = (rew + gamma * m) - qc;
-      const double q1 = qc + alpha * td;
-      q_set(q[u], e, q1);
-      double2* qo = reinterpret_cast<double2*>(a.Q_out + (rb + gidx[u]) * 4);
-      qo[0] = make_double2(q[u][0], q[u][1]);
-      qo[1] = make_double2(q[u][2], q[u][3]);
-      // diagnostic TD on the updated table, spgg.py:446-473
-      const double m2 = sn ? fmax(q[u][2], q[u][3]) : fmax(q[u][0], q[u][1]);
-      const double td2 = (rew + dgamma * m2) - q1;
-      a.atd[rb + gidx[u]] = (float)fabs(dalpha * td2);
+      a.atd[rb + gidx[u]] = td_update<ALG, RNG>(a, pg, rb, gidx[u], t, pkey, eps_t, rew, so, act, sn, q[u], qb[u]);
+      store_q<QB>(a.Q_out, rb + gidx[u], q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -620,6 +783,79 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   }
 }
 
+}  // namespace
+
+namespace spgg_impl {
+
+template <bool M2, bool AS, bool RQ, int RNG, int ALG>
+void launch_t(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
+  constexpr int APT = apt_of(ALG);
+  const dim3 grid(((lc.total_tiles + 7) / 8) * 8);
+#ifndef SPGG_NO_TWC
+  if (lc.tw == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, APT, 40, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
+                       t, fin);
+  else
+#endif
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, APT, 0, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
+                       t, fin);
+}
+
+template <bool M2, bool AS, bool RQ, int ALG>
+void launch_rng(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (lc.rng == SPGG_RNG_PHILOX) launch_t<M2, AS, RQ, SPGG_RNG_PHILOX, ALG>(lc, a, t, fin, s);
+  else launch_t<M2, AS, RQ, SPGG_RNG_MT19937, ALG>(lc, a, t, fin, s);  // INJECT reads the same planes
+}
+
+template <bool M2, bool AS, int ALG>
+void launch_rq(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (lc.rq) launch_rng<M2, AS, true, ALG>(lc, a, t, fin, s);
+  else launch_rng<M2, AS, false, ALG>(lc, a, t, fin, s);
+}
+
+template <int ALG>
+void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (lc.m2) {
+    if (lc.as) launch_rq<true, true, ALG>(lc, a, t, fin, s);
+    else launch_rq<true, false, ALG>(lc, a, t, fin, s);
+  } else {
+    if (lc.as) launch_rq<false, true, ALG>(lc, a, t, fin, s);
+    else launch_rq<false, false, ALG>(lc, a, t, fin, s);
+  }
+}
+
+// Explicit instantiation in the operator's own translation unit; elsewhere
+// an extern declaration keeps the kernels from being instantiated again.
+#define SPGG_LAUNCH_INST(k, name)                                                                   \
+  template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t);
+#define SPGG_LAUNCH_EXTERN(k, name)                                                                 \
+  extern template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t);
+#if SPGG_TU_HAS_ALG(0)
+SPGG_LAUNCH_INST(0, SPGG_ALG_QLEARNING)
+#else
+SPGG_LAUNCH_EXTERN(0, SPGG_ALG_QLEARNING)
+#endif
+#if SPGG_TU_HAS_ALG(1)
+SPGG_LAUNCH_INST(1, SPGG_ALG_SARSA)
+#else
+SPGG_LAUNCH_EXTERN(1, SPGG_ALG_SARSA)
+#endif
+#if SPGG_TU_HAS_ALG(2)
+SPGG_LAUNCH_INST(2, SPGG_ALG_EXPECTED_SARSA)
+#else
+SPGG_LAUNCH_EXTERN(2, SPGG_ALG_EXPECTED_SARSA)
+#endif
+#if SPGG_TU_HAS_ALG(3)
+SPGG_LAUNCH_INST(3, SPGG_ALG_DOUBLE_Q)
+#else
+SPGG_LAUNCH_EXTERN(3, SPGG_ALG_DOUBLE_Q)
+#endif
+
+}  // namespace spgg_impl
+
+#if SPGG_TU_HAS_HOST
+namespace {
+
 // ---------------------------------------------------------------------------
 // Device MT19937, bit-identical to numpy.random.RandomState (legacy seeding,
 // randomkit mt19937_gen + tempering).  One workgroup per replica owns its
@@ -656,9 +892,19 @@ __device__ void mt_twist(uint32_t* mt) {
   __syncthreads();
 }
 
+// Draw program of one iteration, in the reference's order: a segment is
+// rand(L,L) compared with a threshold (2 words per value, "D") or
+// randint(0,2,(L,L)) (1 word, "I"); segment i fills draw plane i.
+//   Q-learning / Expected SARSA: D(eps) I            (algorithms.py:105,108)
+//   SARSA:   D(eps) I D(eps) I D(eps) I              (+ spgg.py:434, 452)
+//   Double-Q: D(eps) I D(0.5)                        (+ algorithms.py:302)
+__host__ __device__ inline int draw_planes(int alg) {
+  return alg == SPGG_ALG_SARSA ? 6 : alg == SPGG_ALG_DOUBLE_Q ? 3 : 2;
+}
+
 __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
-    uint32_t* mt_state, uint8_t* explore, uint8_t* rbit, const double* eps, const double* stats,
-    const int* stop_iter, int n, int slots, int t) {
+    uint32_t* mt_state, uint8_t* draws, size_t plane, const double* eps, const double* stats,
+    const int* stop_iter, int n, int slots, int t, int alg) {
   __shared__ uint32_t mt[624];
   __shared__ uint32_t carry;
   const int rep = blockIdx.x;
@@ -672,9 +918,11 @@ __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
   int pos = (int)gstate[624];
   __syncthreads();
   const double e = eps[(size_t)rep * slots + t];
-  uint8_t* ex = explore + (size_t)rep * n;
-  uint8_t* rb = rbit + (size_t)rep * n;
-  const long long total = 3LL * n, nu = 2LL * n;
+  const int nseg = draw_planes(alg);
+  long long seg_start[7];
+  seg_start[0] = 0;
+  for (int i = 0; i < nseg; ++i) seg_start[i + 1] = seg_start[i] + ((i & 1) ? (long long)n : 2LL * n);
+  const long long total = seg_start[nseg];
   long long produced = 0;
   while (produced < total) {
     if (pos == 624) {
@@ -684,16 +932,21 @@ __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
     const int avail = (int)min((long long)(624 - pos), total - produced);
     if (tid >= pos && tid < pos + avail) {
       const long long w = produced + (tid - pos);
+      int sg = 0;
+      while (w >= seg_start[sg + 1]) ++sg;
+      const long long v = w - seg_start[sg];
+      uint8_t* out = draws + (size_t)sg * plane + (size_t)rep * n;
       const uint32_t y = mt_temper(mt[tid]);
-      if (w < nu) {
-        if ((w & 1) == 0) {
-          if (tid + 1 < pos + avail) ex[w >> 1] = mt_double(y, mt_temper(mt[tid + 1])) < e ? 1 : 0;
+      if ((sg & 1) == 0) {
+        const double thr = (alg == SPGG_ALG_DOUBLE_Q && sg == 2) ? 0.5 : e;
+        if ((v & 1) == 0) {
+          if (tid + 1 < pos + avail) out[v >> 1] = mt_double(y, mt_temper(mt[tid + 1])) < thr ? 1 : 0;
           else carry = y;  // pair straddles the key block
         } else if (tid == pos) {
-          ex[w >> 1] = mt_double(carry, y) < e ? 1 : 0;
+          out[v >> 1] = mt_double(carry, y) < thr ? 1 : 0;
         }
       } else {
-        rb[w - nu] = (uint8_t)(y & 1u);
+        out[v] = (uint8_t)(y & 1u);
       }
     }
     produced += avail;
@@ -755,14 +1008,15 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
   return fail(c, SPGG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Tile shape: <= 1024 agents, rows >= 16 wide when L allows; minimise padded
-// lanes + halo recompute per agent (L=200 -> 40x25, L=1000 -> 40x25).
-void choose_tile(int L, int* TW, int* TH) {
+// Tile shape: <= max_agents (256 threads x agents per thread), rows >= 16
+// wide when L allows; minimise padded lanes + halo recompute per agent
+// (L=200 -> 40x25, L=1000 -> 40x25 at 1024 agents).
+void choose_tile(int L, int max_agents, int* TW, int* TH) {
   int best_w = std::min(L, 32), best_h = std::min(L, 32);
   double best = 1e300;
   for (int w = std::min(L, 16); w <= std::min(L, 56); ++w) {
     for (int h = 1; h <= std::min(L, 64); ++h) {
-      if (w * h > 1024) break;
+      if (w * h > max_agents) break;
       const int tx = (L + w - 1) / w, ty = (L + h - 1) / h;
       const double slots = (double)tx * ty * ((w * h + kBlock - 1) / kBlock) * kBlock;
       const double halo = (double)tx * ty * ((w + 4) * (h + 4) - w * h);
@@ -786,8 +1040,8 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   a.Q_in = c->buf.Q[cur];   a.Q_out = c->buf.Q[nxt];
   a.md_in = c->buf.md[cur]; a.md_out = c->buf.md[nxt];
   a.atd = c->buf.atd;
-  a.explore = c->buf.explore;
-  a.rbit = c->buf.rbit;
+  a.draws = c->buf.draws;
+  a.plane = (size_t)c->buf.draw_plane_stride;
   a.eps = c->buf.eps;
   a.stats = c->buf.stats;
   a.stop_iter = c->buf.stop_iter;
@@ -803,47 +1057,28 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   return a;
 }
 
-template <bool M2, bool AS, bool RQ, int RNG>
-void launch_step_t(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
-  const int total = c->cfg.n_rep * c->tiles_per_rep;
-  const dim3 grid(((total + 7) / 8) * 8);
-#ifndef SPGG_NO_TWC
-  if (c->TW == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
-    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 4, 40>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
-  else
-#endif
-    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 4, 0>), grid, dim3(kBlock), c->lds_bytes, s, a, t, fin);
-}
-
-template <bool M2, bool AS, bool RQ>
-void launch_step_rng(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
-  if (c->cfg.rng_mode == SPGG_RNG_PHILOX) launch_step_t<M2, AS, RQ, SPGG_RNG_PHILOX>(c, a, t, fin, s);
-  else launch_step_t<M2, AS, RQ, SPGG_RNG_MT19937>(c, a, t, fin, s);  // INJECT reads the same bytes
-}
-
-template <bool M2, bool AS>
-void launch_step_rq(const spgg_ctx* c, const TileArgs& a, int t, int fin, hipStream_t s) {
-  if (c->cfg.rep_int8) launch_step_rng<M2, AS, true>(c, a, t, fin, s);
-  else launch_step_rng<M2, AS, false>(c, a, t, fin, s);
-}
-
 void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   const TileArgs a = make_args(c, t);
-  const bool m2 = c->cfg.second_order != 0;
-  const bool as = c->cfg.state_mode == SPGG_STATE_ACTION;
-  if (m2) {
-    if (as) launch_step_rq<true, true>(c, a, t, fin, s);
-    else launch_step_rq<true, false>(c, a, t, fin, s);
-  } else {
-    if (as) launch_step_rq<false, true>(c, a, t, fin, s);
-    else launch_step_rq<false, false>(c, a, t, fin, s);
+  spgg_impl::LaunchCfg lc;
+  lc.m2 = c->cfg.second_order != 0;
+  lc.as = c->cfg.state_mode == SPGG_STATE_ACTION;
+  lc.rq = c->cfg.rep_int8 != 0;
+  lc.rng = c->cfg.rng_mode;
+  lc.tw = c->TW;
+  lc.total_tiles = c->cfg.n_rep * c->tiles_per_rep;
+  lc.lds_bytes = c->lds_bytes;
+  switch (c->cfg.algorithm) {
+    case SPGG_ALG_SARSA: spgg_impl::launch_alg<SPGG_ALG_SARSA>(lc, a, t, fin, s); break;
+    case SPGG_ALG_EXPECTED_SARSA: spgg_impl::launch_alg<SPGG_ALG_EXPECTED_SARSA>(lc, a, t, fin, s); break;
+    case SPGG_ALG_DOUBLE_Q: spgg_impl::launch_alg<SPGG_ALG_DOUBLE_Q>(lc, a, t, fin, s); break;
+    default: spgg_impl::launch_alg<SPGG_ALG_QLEARNING>(lc, a, t, fin, s); break;
   }
 }
 
 void launch_draw(const spgg_ctx* c, int t, hipStream_t s) {
   hipLaunchKernelGGL(spgg_mt_draw_kernel, dim3(c->cfg.n_rep), dim3(kMtThreads), 0, s,
-                     c->buf.mt_state, c->buf.explore, c->buf.rbit, c->buf.eps, c->buf.stats,
-                     c->buf.stop_iter, c->n, c->cfg.iterations + 2, t);
+                     c->buf.mt_state, c->buf.draws, (size_t)c->buf.draw_plane_stride, c->buf.eps,
+                     c->buf.stats, c->buf.stop_iter, c->n, c->cfg.iterations + 2, t, c->cfg.algorithm);
 }
 
 }  // namespace
@@ -851,6 +1086,11 @@ void launch_draw(const spgg_ctx* c, int t, hipStream_t s) {
 extern "C" {
 
 int spgg_abi_version(void) { return SPGG_ABI_VERSION; }
+
+int spgg_draw_planes(int32_t algorithm) {
+  if (algorithm < SPGG_ALG_QLEARNING || algorithm > SPGG_ALG_DOUBLE_Q) return SPGG_E_ARG;
+  return draw_planes(algorithm);
+}
 
 const char* spgg_last_error(const spgg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
@@ -861,23 +1101,25 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     return SPGG_E_ARG;
   if (cfg->state_mode != SPGG_STATE_REPUTATION && cfg->state_mode != SPGG_STATE_ACTION) return SPGG_E_ARG;
   if (cfg->rng_mode < SPGG_RNG_INJECT || cfg->rng_mode > SPGG_RNG_PHILOX) return SPGG_E_ARG;
+  if (cfg->algorithm < SPGG_ALG_QLEARNING || cfg->algorithm > SPGG_ALG_DOUBLE_Q) return SPGG_E_ARG;
+  if (cfg->iterations >= (1 << 26)) return SPGG_E_ARG;  // Philox counter: t + pair*2^26
   if ((long long)cfg->n_rep * cfg->L * cfg->L > (1LL << 31) - 1) return SPGG_E_ARG;
   spgg_ctx* c = new (std::nothrow) spgg_ctx();
   if (!c) return SPGG_E_ARG;
   c->cfg = *cfg;
   c->n = cfg->L * cfg->L;
-  choose_tile(cfg->L, &c->TW, &c->TH);
+  c->apt = spgg_impl::apt_of(cfg->algorithm);
+  choose_tile(cfg->L, kBlock * c->apt, &c->TW, &c->TH);
   if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;
     if (sscanf(e, "%dx%d", &w, &h) == 2 && w >= 1 && h >= 1 && w <= std::min(cfg->L, 56) &&
-        h <= std::min(cfg->L, 64) && w * h <= 1024) {
+        h <= std::min(cfg->L, 64) && w * h <= kBlock * c->apt) {
       c->TW = w;
       c->TH = h;
     }
   }
   c->tiles_x = (cfg->L + c->TW - 1) / c->TW;
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
-  c->apt = (c->TW * c->TH + kBlock - 1) / kBlock <= 2 ? 2 : 4;
   const int HA = cfg->second_order ? 2 : 1;
   const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA, cfg->rep_int8 ? 1 : 8);
   c->lds_bytes = (size_t)ly.bytes;
@@ -918,8 +1160,9 @@ int spgg_bind(spgg_ctx* c, const spgg_buffers* b) {
       return fail(c, SPGG_E_ARG, "spgg_bind: a ping-pong buffer is null");
   if (!b->atd || !b->eps || !b->stats || !b->stop_iter)
     return fail(c, SPGG_E_ARG, "spgg_bind: a required buffer is null");
-  if (c->cfg.rng_mode != SPGG_RNG_PHILOX && (!b->explore || !b->rbit))
-    return fail(c, SPGG_E_ARG, "spgg_bind: explore/rbit buffers required for INJECT/MT19937");
+  if (c->cfg.rng_mode != SPGG_RNG_PHILOX &&
+      (!b->draws || b->draw_plane_stride < (int64_t)c->cfg.n_rep * c->n))
+    return fail(c, SPGG_E_ARG, "spgg_bind: draw planes (stride >= n_rep*n) required for INJECT/MT19937");
   if (c->cfg.rng_mode == SPGG_RNG_MT19937 && !b->mt_state)
     return fail(c, SPGG_E_ARG, "spgg_bind: mt_state required for MT19937");
   if (((reinterpret_cast<uintptr_t>(b->Q[0]) | reinterpret_cast<uintptr_t>(b->Q[1])) & 15) != 0)
@@ -989,3 +1232,4 @@ int spgg_destroy(spgg_ctx* c) {
 }
 
 }  // extern "C"
+#endif  // SPGG_TU_HAS_HOST

@@ -9,9 +9,10 @@ reference's HDF5 datasets (`src/model/spgg.py:594-633`) by `histories()`.
 
 Random streams:
   * "mt19937": init draws on the host exactly as SPGG.__init__ does
-    (spgg.py:121,162) from `numpy.random.RandomState`; the continuing MT19937
-    key is moved to the device, which draws every step's rand(L,L) and
-    randint(0,2,(L,L)) (algorithms.py:105,108) bit-identically.
+    (spgg.py:121-127,162) from `numpy.random.RandomState`; the continuing
+    MT19937 key is moved to the device, which draws every step's rand(L,L)
+    and randint(0,2,(L,L)) (algorithms.py:105,108) -- plus SARSA's two
+    further selects and Double-Q's table choice -- bit-identically.
   * "inject": the host draws each step (tests / debugging).
   * "philox": counter-based per-agent stream; statistical parity only.
 """
@@ -27,6 +28,7 @@ import numpy as np
 import torch
 
 from . import _lib as C
+from .algorithms import canonical_name
 
 SNAPSHOT_ITERS = (1, 10, 100, 1000, 5000, 10000, 20000, 30000, 40000)  # spgg.py:153
 PNG_ITERS = set(SNAPSHOT_ITERS) | {5000}                                 # spgg.py:553
@@ -129,17 +131,26 @@ def epsilon_table(eps0, decay, emin, n):
 class InitState:
     Q: np.ndarray                 # (L, L, 2, 2) float64
     S: np.ndarray                 # (L, L) int
+    tables: Optional[tuple] = None       # Double-Q: (q_table_1, q_table_2), each (L, L, 2, 2)
     mt_key: Optional[np.ndarray] = None  # (624,) uint32 continuing MT19937 key
     mt_pos: int = 0
     rs: Optional[np.random.RandomState] = None  # host stream (inject mode)
 
 
-def reference_init(L: int, rs: np.random.RandomState, S_in_one=None) -> InitState:
-    """SPGG.__init__'s draws: Q ~ U(-0.01, 0.01) then S ~ randint(0,2) (spgg.py:121,162)."""
+def reference_init(L: int, rs: np.random.RandomState, S_in_one=None, algorithm="qlearning") -> InitState:
+    """SPGG.__init__'s draws: Q ~ U(-0.01, 0.01) (spgg.py:121), for Double-Q two
+    more tables whose mean replaces Q (spgg.py:124-127, algorithms.py:250-266),
+    then S ~ randint(0,2) (spgg.py:162)."""
     Q = rs.uniform(low=-0.01, high=0.01, size=(L, L, 2, 2))
+    tables = None
+    if canonical_name(algorithm) == "double_qlearning":
+        q1 = rs.uniform(low=-0.01, high=0.01, size=(L, L, 2, 2))
+        q2 = rs.uniform(low=-0.01, high=0.01, size=(L, L, 2, 2))
+        tables, Q = (q1, q2), (q1 + q2) / 2
     S = rs.randint(0, 2, size=(L, L)) if S_in_one is None else np.asarray(S_in_one)
     st = rs.get_state()
-    return InitState(Q=Q, S=S, mt_key=np.asarray(st[1], dtype=np.uint32), mt_pos=int(st[2]), rs=rs)
+    return InitState(Q=Q, S=S, tables=tables, mt_key=np.asarray(st[1], dtype=np.uint32),
+                     mt_pos=int(st[2]), rs=rs)
 
 
 class BatchEngine:
@@ -148,7 +159,8 @@ class BatchEngine:
     def __init__(self, L: int, iterations: int, replicas: Sequence[ReplicaParams],
                  use_second_order: bool = True, state_representation: str = "reputation",
                  rng: str = "mt19937", device=None, init: Optional[Sequence[InitState]] = None,
-                 lib_path: Optional[str] = None, streams: Optional[int] = None):
+                 lib_path: Optional[str] = None, streams: Optional[int] = None,
+                 algorithm: str = "qlearning"):
         if state_representation not in ("reputation", "action"):
             raise ValueError(f"Unknown state_representation: {state_representation}. "
                              f"Must be 'reputation' or 'action'")
@@ -157,6 +169,10 @@ class BatchEngine:
         if not torch.cuda.is_available():
             raise C.SpggError("BatchEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.lib = C.load(lib_path)
+        self.algorithm = canonical_name(algorithm)
+        self.alg = C.ALGORITHMS[self.algorithm]
+        self.double_q = self.alg == C.ALG_DOUBLE_Q
+        self.QW = 8 if self.double_q else 4     # doubles per agent in the Q buffers
         self.L, self.n = int(L), int(L) * int(L)
         self.T = int(iterations)
         self.reps = list(replicas)
@@ -166,7 +182,8 @@ class BatchEngine:
         self.rng = rng
         self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         if init is None:
-            init = [reference_init(self.L, np.random.RandomState(p.seed)) for p in self.reps]
+            init = [reference_init(self.L, np.random.RandomState(p.seed), algorithm=self.algorithm)
+                    for p in self.reps]
         self.init = list(init)
         if len(self.init) != self.R:
             raise ValueError("one InitState per replica")
@@ -196,7 +213,13 @@ class BatchEngine:
         R, n, T, d = self.R, self.n, self.T, self.dev
         f64, u8 = torch.float64, torch.uint8
         S0 = np.stack([np.asarray(s.S).reshape(n) for s in self.init]).astype(np.uint8)
-        Q0 = np.stack([np.asarray(s.Q, dtype=np.float64).reshape(n, 4) for s in self.init])
+        if self.double_q:
+            if any(s.tables is None for s in self.init):
+                raise ValueError("double_qlearning needs both initial tables (InitState.tables)")
+            Q0 = np.stack([np.concatenate([np.asarray(t, dtype=np.float64).reshape(n, 4) for t in s.tables],
+                                          axis=1) for s in self.init])
+        else:
+            Q0 = np.stack([np.asarray(s.Q, dtype=np.float64).reshape(n, 4) for s in self.init])
         self.S = torch.zeros((2, R, n), dtype=u8, device=d)
         self.S[0].copy_(torch.from_numpy(S0))
         units = [p.rep_unit() for p in self.reps]
@@ -204,12 +227,14 @@ class BatchEngine:
                          and os.environ.get("SPGG_REP_F64", "0") != "1")
         self.rep_units = np.array([u if u is not None else 1.0 for u in units])
         self.Rep = torch.zeros((2, R, n), dtype=torch.int8 if self.rep_int8 else f64, device=d)
-        self.Qb = torch.zeros((2, R, n, 4), dtype=f64, device=d)
+        self.Qb = torch.zeros((2, R, n, self.QW), dtype=f64, device=d)
         self.Qb[0].copy_(torch.from_numpy(Q0))
         self.md = torch.zeros((2, R, n), dtype=f64, device=d)
         self.atd = torch.zeros((R, n), dtype=torch.float32, device=d)
-        self.explore = torch.zeros((R, n), dtype=u8, device=d)
-        self.rbit = torch.zeros((R, n), dtype=u8, device=d)
+        # draw planes of one iteration (device MT19937 / inject), spgg_abi.h
+        self.n_planes = C.DRAW_PLANES[self.alg]
+        shape = (self.n_planes, R, n) if self.rng != "philox" else (1, 1, 1)
+        self.draws = torch.zeros(shape, dtype=u8, device=d)
         mt = np.zeros((R, 625), dtype=np.uint32)
         if self.rng == "mt19937":
             for k, s in enumerate(self.init):
@@ -236,7 +261,8 @@ class BatchEngine:
     def _create(self):
         cfg = C.Config(device=self.dev.index, n_rep=self.R, L=self.L, second_order=int(self.M2),
                        state_mode=C.STATE_ACTION if self.state_rep == "action" else C.STATE_REPUTATION,
-                       rng_mode=C.RNG_MODES[self.rng], iterations=self.T, rep_int8=int(self.rep_int8))
+                       rng_mode=C.RNG_MODES[self.rng], iterations=self.T, rep_int8=int(self.rep_int8),
+                       algorithm=self.alg)
         params = [p.to_c() for p in self.reps]
         for k, p in enumerate(params):
             p.stream_id = k
@@ -254,7 +280,8 @@ class BatchEngine:
                 b.S[i], b.R[i] = self.S[i][r0].data_ptr(), self.Rep[i][r0].data_ptr()
                 b.Q[i], b.md[i] = self.Qb[i][r0].data_ptr(), self.md[i][r0].data_ptr()
             b.atd = self.atd[r0].data_ptr()
-            b.explore, b.rbit = self.explore[r0].data_ptr(), self.rbit[r0].data_ptr()
+            b.draws = self.draws[0, min(r0, self.draws.shape[1] - 1)].data_ptr()
+            b.draw_plane_stride = self.draws.shape[1] * self.draws.shape[2]
             b.mt_state = self.mt_state[r0].data_ptr()
             b.eps, b.stats = self.eps[r0].data_ptr(), self.stats[r0].data_ptr()
             b.stop_iter = self.stop_iter[r0].data_ptr()
@@ -300,20 +327,25 @@ class BatchEngine:
 
     # -- stepping ------------------------------------------------------------
     def _inject(self, t):
-        """Host draws of iteration t (algorithms.py:105,108) for replicas that execute it."""
+        """Host draws of iteration t, in the reference's order, for replicas that
+        execute it: every select draws rand then randint (algorithms.py:105,108);
+        SARSA selects three times (spgg.py:410,434,452); Double-Q then draws its
+        table choice (algorithms.py:302)."""
         ncoop = self.stats[:, t, C.ST_NCOOP].cpu().numpy()
         stop = self.stop_iter.cpu().numpy()
-        ex = np.zeros((self.R, self.n), dtype=np.uint8)
-        rb = np.zeros((self.R, self.n), dtype=np.uint8)
+        planes = np.zeros((self.n_planes, self.R, self.n), dtype=np.uint8)
+        L = self.L
         for k, s in enumerate(self.init):
             if stop[k] != 0 or ncoop[k] == 0 or ncoop[k] == self.n:
                 continue
-            u = s.rs.rand(self.L, self.L).reshape(-1)
-            b = s.rs.randint(0, 2, size=(self.L, self.L)).reshape(-1)
-            ex[k] = u < self.eps_host[k, t]
-            rb[k] = b
-        self.explore.copy_(torch.from_numpy(ex))
-        self.rbit.copy_(torch.from_numpy(rb))
+            e = self.eps_host[k, t]
+            selects = 3 if self.alg == C.ALG_SARSA else 1
+            for j in range(selects):
+                planes[2 * j, k] = s.rs.rand(L, L).reshape(-1) < e
+                planes[2 * j + 1, k] = s.rs.randint(0, 2, size=(L, L)).reshape(-1)
+            if self.double_q:
+                planes[2, k] = s.rs.rand(L, L).reshape(-1) < 0.5
+        self.draws.copy_(torch.from_numpy(planes))
 
     def step(self, n_steps: int):
         """Enqueue the next n_steps iterations (no host sync except in inject mode)."""
@@ -399,10 +431,23 @@ class BatchEngine:
         else:   # S_{last+1}, R_{last+1}; Q finalized by the flush launch last+1
             cur, qb = last & 1, (last + 1) & 1
         L = self.L
-        Q = self.Qb[qb, k].cpu().numpy().reshape(L, L, 2, 2)
+        Qk = self.Qb[qb, k].cpu().numpy()
+        if self.double_q:   # q_table = mean of the two tables (algorithms.py:262-266)
+            Q = ((Qk[:, :4] + Qk[:, 4:]) / 2).reshape(L, L, 2, 2)
+        else:
+            Q = Qk.reshape(L, L, 2, 2)
         R = self._rep_host(cur)[k].reshape(L, L)
         S = (self.S[cur, k].cpu().numpy() & 1).reshape(L, L).astype(np.int64)
         return Q, R, S
+
+    def final_tables(self, k):
+        """Double-Q: (q_table_1, q_table_2) of replica k after the run."""
+        if not self.double_q:
+            raise ValueError("final_tables: not a double_qlearning engine")
+        s = int(self.stopped[k])
+        qb = s & 1 if s else self.last_iteration(k) + 1 & 1
+        Qk = self.Qb[qb, k].cpu().numpy()
+        return Qk[:, :4].reshape(self.L, self.L, 2, 2).copy(), Qk[:, 4:].reshape(self.L, self.L, 2, 2).copy()
 
     def _rep_host(self, buf):
         """R plane `buf` of every replica as float64 (exact k*unit in compact mode)."""

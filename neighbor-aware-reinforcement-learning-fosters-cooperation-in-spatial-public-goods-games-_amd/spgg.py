@@ -106,9 +106,7 @@ class SPGG:
 
         Returns (final_coop_rate, final_def_rate, mean_payoff) as numpy float64.
         """
-        if type(self.algorithm) is not A.QLearning and getattr(self.algorithm, "kind", "") != "qlearning":
-            raise NotImplementedError(
-                f"{type(self.algorithm).__name__}: only Q-learning runs on the HIP path so far")
+        kind = A.canonical_name(self.algorithm)
         L = self.L
         S0 = np.asarray(self._Sn)
         n0 = int(np.sum(S0 == 0))
@@ -120,12 +118,17 @@ class SPGG:
                                  f"Must be 'reputation' or 'action'")
             state_rep = 'reputation'
         g = np.random.get_state()
-        init = InitState(Q=np.asarray(self.q_table, dtype=np.float64), S=S0,
+        tables = None
+        if kind == "double_qlearning":
+            tables = (np.asarray(self.algorithm.q_table_1, dtype=np.float64),
+                      np.asarray(self.algorithm.q_table_2, dtype=np.float64))
+        init = InitState(Q=np.asarray(self.q_table, dtype=np.float64), S=S0, tables=tables,
                          mt_key=np.asarray(g[1], dtype=np.uint32), mt_pos=int(g[2]))
         iters = int(self.iterations)
         eng = BatchEngine(L, max(iters, 1), [self._replica_params()],
                           use_second_order=bool(self.use_second_order),
-                          state_representation=state_rep, rng="mt19937", init=[init])
+                          state_representation=state_rep, rng="mt19937", init=[init],
+                          algorithm=kind)
         if iters < 1:
             eng.T = 0
         snapshots_dir = os.path.join(self.folder, 'plots', 'snapshots') if self.folder else 'snapshots'
@@ -134,6 +137,7 @@ class SPGG:
             eng.run(snapshots=True, png=self.save_png)
             hist = eng.histories()[0]
             Q, R, S = eng.final_state(0)
+            tables = eng.final_tables(0) if kind == "double_qlearning" else None
             last = eng.last_iteration(0)
             P = eng.payoff_at(last)[0] if last >= 1 else None
             key, pos = eng.mt_state_host(0)
@@ -183,6 +187,8 @@ class SPGG:
 
         # state after the run, as the reference leaves it
         self.q_table, self.R, self._Sn = Q, R, S
+        if tables is not None:  # the operator's own tables (spgg.py:496-502)
+            self.algorithm.q_table_1, self.algorithm.q_table_2 = tables
         self._S = [(S == j).astype(int) for j in range(self.num_of_strategies)]
         self.cache = {}
         if P is not None:

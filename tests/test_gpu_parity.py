@@ -33,7 +33,11 @@ def _pinned_model(c):
         if c.S_in_one is not None:
             kw["S_in_one"] = c.S_in_one
         if c.algorithm_instance:
-            kw["algorithm"] = spgg_amd.QLearning(**c.algorithm_instance)
+            alg = dict(c.algorithm_instance)
+            cls = {"qlearning": spgg_amd.QLearning, "sarsa": spgg_amd.SARSA,
+                   "expected_sarsa": spgg_amd.ExpectedSARSA,
+                   "double_qlearning": spgg_amd.DoubleQLearning}[alg.pop("kind", "qlearning")]
+            kw["algorithm"] = cls(**alg)
         return spgg_amd.SPGG(**kw)
     finally:
         np.random.seed = orig
@@ -61,10 +65,13 @@ def test_spgg_dropin_matches_reference(name, tmp_path):
     assert np.array_equal(m._Sn, c.Sn)
     assert np.array_equal(np.array(ret, dtype=float), c.ret)
     assert m.algorithm.epsilon == c.epsilon
+    if c.tables is not None:   # Double-Q's own tables
+        assert np.array_equal(m.algorithm.q_table_1, c.tables[0])
+        assert np.array_equal(m.algorithm.q_table_2, c.tables[1])
 
 
-def _oracle_final(L, T, p, seed, M2, state):
-    op = O.Params(L=L, iterations=T, use_second_order=M2, state_representation=state,
+def _oracle_final(L, T, p, seed, M2, state, algorithm="qlearning"):
+    op = O.Params(L=L, iterations=T, use_second_order=M2, state_representation=state, algorithm=algorithm,
                   **{k: getattr(p, k) for k in ("r", "c", "cost", "alpha", "gamma", "epsilon",
                                                  "epsilon_decay", "epsilon_min", "influence_factor",
                                                  "lambda_epsilon", "delta_R_D", "R_min", "R_max",
@@ -100,12 +107,43 @@ def test_batched_replicas_match_oracle(M2, state):
     eng.close()
 
 
-def test_device_mt19937_equals_host_injection():
+ALGS = ["qlearning", "sarsa", "expected_sarsa", "double_qlearning"]
+
+
+@pytest.mark.parametrize("alg", ALGS[1:])
+@pytest.mark.parametrize("M2,state", [(False, "reputation"), (True, "action"), (True, "reputation")])
+def test_batched_operators_match_oracle(alg, M2, state):
+    """SARSA / Expected SARSA / Double-Q batches, device MT19937, vs the oracle bit for bit."""
+    L, T = 18, 50
+    reps = [_runner_params(r=r, influence_factor=k, seed=s)
+            for r, k, s in [(2.5, 0.0, 11), (3.0, 1.0, 12), (4.2, 0.5, 13), (1.0, 1.5, 14)]]
+    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng="mt19937",
+                      algorithm=alg)
+    eng.run(snapshots=False)
+    hs = eng.histories()
+    for k, p in enumerate(reps):
+        ds, fin = _oracle_final(L, T, p, p.seed, M2, state, alg)
+        Q, R, S = eng.final_state(k)
+        assert np.array_equal(Q, fin["Q"]), k
+        assert np.array_equal(R, fin["R"]), k
+        assert np.array_equal(S, fin["S"]), k
+        if alg == "double_qlearning":
+            q1, q2 = eng.final_tables(k)
+            assert np.array_equal(q1, fin["tables"][0]) and np.array_equal(q2, fin["tables"][1]), k
+        for key in ("coop_rate_history", "switch_C_to_D", "switch_D_to_C"):
+            assert np.array_equal(hs[k][key], ds[key]), (k, key)
+        for key in ("neighbor_influence_percent", "avg_q_s0_c_history", "avg_q_s1_d_history"):
+            np.testing.assert_allclose(hs[k][key], ds[key], err_msg=key, **FLOAT_TOL)
+    eng.close()
+
+
+@pytest.mark.parametrize("alg", ALGS)
+def test_device_mt19937_equals_host_injection(alg):
     L, T = 24, 40
     reps = [_runner_params(seed=s) for s in (10, 11, 12)]
     outs = []
     for rng in ("mt19937", "inject"):
-        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng)
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, algorithm=alg)
         eng.run(snapshots=False)
         outs.append([eng.final_state(k) for k in range(len(reps))])
         eng.close()
@@ -114,22 +152,30 @@ def test_device_mt19937_equals_host_injection():
             assert np.array_equal(x, y)
 
 
-def test_device_mt_stream_matches_numpy():
-    """spgg_draw: the device key reproduces RandomState.rand/randint bytes exactly."""
-    L, T = 37, 3   # 3*37^2 words: several key blocks with a straddling pair
+@pytest.mark.parametrize("alg", ALGS)
+def test_device_mt_stream_matches_numpy(alg):
+    """spgg_draw: the device key reproduces every RandomState draw of a step exactly
+    (odd L: pairs straddle key blocks and draw segments start at odd words)."""
+    L, T = 37, 3
     reps = [_runner_params(seed=7, epsilon=0.5)]
-    eng = BatchEngine(L, T, reps, use_second_order=False, rng="mt19937")
+    eng = BatchEngine(L, T, reps, use_second_order=False, rng="mt19937", algorithm=alg)
     rs = np.random.RandomState(7)
-    rs.uniform(-0.01, 0.01, (L, L, 2, 2)); rs.randint(0, 2, (L, L))
+    reference_init(L, rs, algorithm=alg)
     lib = eng.lib
     from spgg_amd import _lib as C
     eng.stats[:, :, C.ST_NCOOP] = 1.0   # no iteration is absorbing: every draw happens
     for t in (1, 2, 3):
         C.check(lib.spgg_draw(eng.ctx, t, eng.stream), eng.ctx, "spgg_draw")
-        u = rs.rand(L, L).reshape(-1)
-        b = rs.randint(0, 2, (L, L)).reshape(-1)
-        assert np.array_equal(eng.explore[0].cpu().numpy(), (u < eng.eps_host[0, t]).astype(np.uint8))
-        assert np.array_equal(eng.rbit[0].cpu().numpy(), b.astype(np.uint8))
+        d = O.draw_step(rs, L, alg)
+        e = eng.eps_host[0, t]
+        want = [d["u"] < e, d["b"]]
+        if alg == "sarsa":
+            want += [d["u2"] < e, d["b2"], d["u3"] < e, d["b3"]]
+        if alg == "double_qlearning":
+            want += [d["u_upd"] < 0.5]
+        assert eng.draws.shape[0] == len(want)
+        for p_, w in enumerate(want):
+            assert np.array_equal(eng.draws[p_, 0].cpu().numpy(), w.reshape(-1).astype(np.uint8)), (t, p_)
     eng.close()
 
 
@@ -190,14 +236,15 @@ def test_nondyadic_and_dyadic_reputation_vs_oracle(gain, loss, rmin, rmax):
     eng.close()
 
 
-@pytest.mark.parametrize("rng", ["philox", "mt19937"])
-def test_replica_groups_on_streams_match_single_stream(rng):
+@pytest.mark.parametrize("rng,alg", [("philox", "qlearning"), ("mt19937", "qlearning"),
+                                     ("philox", "sarsa"), ("philox", "double_qlearning")])
+def test_replica_groups_on_streams_match_single_stream(rng, alg):
     """Splitting the batch over concurrent streams changes nothing bit-wise."""
     L, T = 30, 60
     reps = [_runner_params(r=2.0 + 0.25 * s, seed=s) for s in range(9)]
     res = {}
     for G in (1, 3, 4):
-        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=G)
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=G, algorithm=alg)
         assert eng.G == G
         eng.run(snapshots=False)
         res[G] = ([eng.final_state(k) for k in range(len(reps))], eng.stats.cpu().numpy(),

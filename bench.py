@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--rng", default="philox", choices=["philox", "mt19937"])
     ap.add_argument("--streams", type=int, default=None,
                     help="replica groups on concurrent HIP streams (default: auto)")
+    ap.add_argument("--replicas", type=int, default=None,
+                    help="experiment: first N replicas of the workload grid (cycled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
@@ -128,6 +130,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     desc, L, M2, state, reps = workload(args.config, rank)
+    if args.replicas:
+        import dataclasses
+        reps = [dataclasses.replace(reps[i % len(reps)], seed=(reps[i % len(reps)].seed or 0) + 7919 * (i // len(reps)))
+                for i in range(args.replicas)]
+        desc += f" [experiment: {args.replicas} replicas]"
     K, W = args.steps, args.warmup
     T = K + W
     eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng,

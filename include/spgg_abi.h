@@ -19,7 +19,7 @@
  * Conventions: every function returns 0 on success, a negative SPGG_E* code on
  * failure (detail in spgg_last_error).  No C++ exception crosses the ABI.
  * One iteration is ONE kernel launch over all replicas (plus one MT19937 draw
- * launch in that mode).
+ * launch in that mode; plus one prologue launch before iteration 1).
  * Buffers are DEVICE pointers owned by the caller (e.g. torch tensors); the
  * library only allocates its per-replica parameter table and frees it in
  * spgg_destroy.  A context is bound to one device and is not thread-safe.
@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 6
+#define SPGG_ABI_VERSION 7
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -54,7 +54,7 @@ extern "C" {
 /* random stream used by the eps-greedy selects */
 #define SPGG_RNG_INJECT 0   /* caller fills the draw planes per step (host MT19937 etc.) */
 #define SPGG_RNG_MT19937 1  /* device MT19937, bit-identical to numpy.random.RandomState */
-#define SPGG_RNG_PHILOX 2   /* counter-based Philox4x32-10 keyed by (seed, replica, step, agent) */
+#define SPGG_RNG_PHILOX 2   /* counter-based Philox2x32-10 keyed by (seed, replica), counter (agent, step) */
 
 /* Per-step history record: stats[rep][t][SPGG_NSTAT] (float64), t = 0 .. iterations+1.
  * Integer counts are stored exactly as float64. */
@@ -133,19 +133,26 @@ typedef struct {
   double norm_rcp;    /* 1/norm_den rounded to nearest (host) */
 } spgg_rep_params;
 
-/* Device buffers, all replica-major.  n = L*L.  Ping-pong pairs are indexed
- * by iteration parity: iteration t reads [ (t-1)&1 ] and writes [ t&1 ].
- *   S[2]      uint8  [n_rep][n]      bit0: strategy S_t (0 = C); bits 1-3: the
- *                                    deferred-NI record of iteration t-1
- *                                    (s_old, a*==a, prev strategy)
- *   R[2]      f64    [n_rep][n]      reputation R_t (int8 R_t/rep_unit if rep_int8)
- *   Q[2]      f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2);
- *                                    Q[(t-1)&1] holds iteration t-1's TD update
- *                                    without its NI term (applied by iteration t).
+/* Device buffers, all replica-major.  n = L*L.
+ *   S[2]      uint8  [n_rep][n]      S_t in S[(t-1) & 1] (iteration t reads [(t-1)&1],
+ *                                    writes [t&1]).  bit0: strategy (0 = C); bits 1-4:
+ *                                    bookkeeping of iteration t-1 (s_old, best
+ *                                    neighbour's action matched, previous strategy,
+ *                                    new state s_t)
+ *   R[2]      f64    [n_rep][n]      reputation R_t in R[(t-1) & 1] (int8 R_t/rep_unit
+ *                                    if rep_int8)
+ *   Q         f64    [n_rep][n][2][2] q_table in the reference layout (L,L,2,2),
+ *                                    updated IN PLACE: between launches it holds the
+ *                                    last iteration's TD update without its NI term
+ *                                    (applied by the next launch / spgg_flush).
  *                                    Double Q-learning: [n_rep][n][2][2][2] =
  *                                    q_table_1[s][a] then q_table_2[s][a] per agent
- *   md[2]     f64    [n_rep][n]      max(0, max_diff) of iteration t-1
- *   atd       f32    [n_rep][n]      |alpha*td'| of the pending iteration (diagnostic)
+ *   pub[2]    f64    [n_rep][spgg_pub_doubles]  border records (library-internal
+ *                                    layout): the Q row of the next state and
+ *                                    max(0, max_diff) of every agent within M cells of
+ *                                    its tile's edge, read by the neighbouring tiles
+ *   md        f64    [n_rep][n]      max(0, max_diff) of the pending iteration, in place
+ *   atd       f32    [n_rep][n]      |alpha*td'| of the pending iteration (diagnostic), in place
  *   draws     uint8  [planes][..][n] the step's random draws as 0/1 bytes (INJECT/MT19937),
  *                                    one plane per draw of the reference, in its order
  *                                    (spgg_draw_planes): plane 2k = (rand < eps) and
@@ -159,16 +166,17 @@ typedef struct {
  *   stats     f64    [n_rep][iterations+2][SPGG_NSTAT]  zero-initialised; slot
  *                                    t0 must hold NCOOP of S_t0 before stepping
  *   stop_iter int32  [n_rep]         0 while running, else the absorbing iteration
- * Initial state: S[0] = population (bits 1-3 zero), R[0] = 0, Q[0] = initial table.
- * Final state of a replica absorbed at s: S,R in [(s-1)&1], Q in [s&1]; of a
- * replica still running after spgg_flush(t_last): S,R in [t_last&1], Q in
- * [(t_last+1)&1].
+ * Initial state: S[0] = population (bits 1-7 zero), R[0] = 0, Q = initial table.
+ * Final state of a replica absorbed at s: S, R in [(s-1)&1]; of a replica still
+ * running after spgg_flush(t_last): S, R in [t_last&1].  Q (in place) is final
+ * after spgg_flush / the absorbing launch.
  */
 typedef struct {
   uint8_t* S[2];
   void* R[2];     /* double, or int8_t when spgg_config.rep_int8 */
-  double* Q[2];
-  double* md[2];
+  double* Q;
+  double* pub[2];
+  double* md;
   float* atd;
   uint8_t* draws;
   int64_t draw_plane_stride;  /* bytes between draw planes (>= n_rep*n) */
@@ -204,6 +212,9 @@ int spgg_draw(spgg_ctx* ctx, int32_t t, void* hip_stream);
 /* P (normalised payoff, spgg.py:373-378) of every agent from S_t into
  * out[n_rep][n] (device).  Used for SPGG.P and run()'s return value. */
 int spgg_payoff(spgg_ctx* ctx, int32_t t, double* out, void* hip_stream);
+
+/* Doubles per replica of each border-record buffer (spgg_buffers.pub). */
+int spgg_pub_doubles(const spgg_ctx* ctx, int64_t* per_rep);
 
 /* Tile shape (agents) the step kernel uses for this lattice. */
 int spgg_tile_shape(const spgg_ctx* ctx, int32_t* tw, int32_t* th);

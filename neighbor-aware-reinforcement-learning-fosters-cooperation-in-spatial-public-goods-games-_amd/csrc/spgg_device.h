@@ -9,7 +9,13 @@
 
 namespace spgg {
 
-constexpr int kBlock = 256;
+// Threads per step-kernel workgroup (a tile holds up to 1024 agents: 4 per
+// thread at 256, 2 at 512).  Build knob for A/B timing: -DSPGG_BLOCK=512.
+#ifndef SPGG_BLOCK
+#define SPGG_BLOCK 256
+#endif
+constexpr int kBlock = SPGG_BLOCK;
+static_assert(kBlock == 256 || kBlock == 512, "SPGG_BLOCK must be 256 or 512");
 constexpr int kWaves = kBlock / 64;
 
 __device__ __forceinline__ int wrap(int x, int L) {
@@ -52,16 +58,36 @@ __device__ __forceinline__ double swap_sum(double a, double b) {
   return __hiloint2double(ahi, alo) + __hiloint2double(bhi, blo);
 }
 
+// Same exchanges for packed integer counters (one dword per value).
 template <int MASK>
-__device__ __forceinline__ double partner(double x) {
-  if constexpr (MASK == 8) return dpp_f64<0x128>(x);   // row_ror:8      -> l^8
-  else if constexpr (MASK == 4) return dpp_f64<0x141>(x);  // row_half_mirror -> l^7
-  else if constexpr (MASK == 2) return dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
-  else return dpp_f64<0xB1>(x);                            // quad_perm [1,0,3,2]
+__device__ __forceinline__ uint32_t swap_sum(uint32_t a, uint32_t b) {
+  const auto s = MASK == 32 ? __builtin_amdgcn_permlane32_swap((int)a, (int)b, false, false)
+                            : __builtin_amdgcn_permlane16_swap((int)a, (int)b, false, false);
+  return (uint32_t)s[0] + (uint32_t)s[1];
 }
 
-template <int CNT, int MASK, int K>
-__device__ __forceinline__ void transpose_level(double (&v)[K], int lane) {
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+
+template <int MASK, typename T>
+__device__ __forceinline__ T partner(T x) {
+  if constexpr (sizeof(T) == 8) {
+    if constexpr (MASK == 8) return dpp_f64<0x128>(x);        // row_ror:8      -> l^8
+    else if constexpr (MASK == 4) return dpp_f64<0x141>(x);   // row_half_mirror -> l^7
+    else if constexpr (MASK == 2) return dpp_f64<0x4E>(x);    // quad_perm [2,3,0,1]
+    else return dpp_f64<0xB1>(x);                             // quad_perm [1,0,3,2]
+  } else {
+    if constexpr (MASK == 8) return dpp_u32<0x128>(x);
+    else if constexpr (MASK == 4) return dpp_u32<0x141>(x);
+    else if constexpr (MASK == 2) return dpp_u32<0x4E>(x);
+    else return dpp_u32<0xB1>(x);
+  }
+}
+
+template <int CNT, int MASK, int K, typename T>
+__device__ __forceinline__ void transpose_level(T (&v)[K], int lane) {
   if constexpr (MASK >= 1) {
     constexpr int h = CNT > 1 ? CNT / 2 : 1;
     if constexpr (MASK >= 16) {
@@ -76,15 +102,15 @@ __device__ __forceinline__ void transpose_level(double (&v)[K], int lane) {
         const bool upper = (lane & MASK) != 0;
 #pragma unroll
         for (int i = 0; i < h; ++i) {
-          const double send = upper ? v[i] : v[i + h];
-          const double keep = upper ? v[i + h] : v[i];
+          const T send = upper ? v[i] : v[i + h];
+          const T keep = upper ? v[i + h] : v[i];
           v[i] = keep + partner<MASK>(send);
         }
       } else {
         v[0] += partner<MASK>(v[0]);
       }
     }
-    transpose_level<(CNT > 1 ? CNT / 2 : 1), MASK / 2, K>(v, lane);
+    transpose_level<(CNT > 1 ? CNT / 2 : 1), MASK / 2, K, T>(v, lane);
   }
 }
 
@@ -93,7 +119,7 @@ __device__ __forceinline__ void transpose_level(double (&v)[K], int lane) {
 template <int K>
 __device__ __forceinline__ double block_reduce(double (&v)[K], double* lds) {
   static_assert(K >= 1 && K <= 64 && (K & (K - 1)) == 0, "K must be a power of two");
-  transpose_level<K, 32, K>(v, threadIdx.x & 63);
+  transpose_level<K, 32, K, double>(v, threadIdx.x & 63);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int per = 64 / K;
   if ((lane & (per - 1)) == 0) lds[wave * K + lane / per] = v[0];
@@ -149,8 +175,8 @@ __device__ __forceinline__ uint2 philox2x32_10(uint2 c, uint32_t k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r) k += 0x9E3779B9u;
-    const uint32_t lo = 0xD256D193u * c.x, hi = __umulhi(0xD256D193u, c.x);
-    c = make_uint2(hi ^ k ^ c.y, lo);
+    const uint64_t p = (uint64_t)0xD256D193u * c.x;  // one v_mad_u64_u32 for lo and hi
+    c = make_uint2((uint32_t)(p >> 32) ^ k ^ c.y, (uint32_t)p);
   }
   return c;
 }

@@ -44,7 +44,8 @@ using namespace spgg;
 
 // Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
-//   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor)
+//   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
+//   128 = memory only (the owned loads, staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
@@ -62,27 +63,28 @@ using namespace spgg;
 namespace spgg_impl {
 
 struct TileArgs {
-  const uint8_t* S_in;  // S_t   (bit0 strategy, bits1-3 pending-NI bookkeeping)
-  uint8_t* S_out;       // S_{t+1}
-  const void* R_in;     // f64, or int8 units of rep_unit (compact reputation)
+  const uint8_t* S_in;    // S_t   (bit0 strategy, bits1-4 bookkeeping of iteration t-1)
+  uint8_t* S_out;         // S_{t+1}
+  const void* R_in;       // f64, or int8 units of rep_unit (compact reputation)
   void* R_out;
-  const double* Q_in;   // [rep][n][4]: after TD of t-1, before its NI term
-  double* Q_out;
-  const double* md_in;  // max(0, max_diff) of t-1
-  double* md_out;
-  float* atd;           // |alpha*td'| of the pending iteration (owner only)
-  const uint8_t* draws;  // draw planes (INJECT / MT19937), plane stride `plane`
+  double* Q;              // [rep][n][QW], IN PLACE: after TD of t-1, before its NI term
+  double* md;             // [rep][n], IN PLACE: max(0, max_diff) of iteration t-1
+  const double* pub_in;   // border records of iteration t-1 (ring recompute reads them)
+  double* pub_out;        // border records of iteration t
+  float* atd;             // [rep][n], IN PLACE: |alpha*td'| of iteration t-1 (diagnostic)
+  const uint8_t* draws;   // draw planes (INJECT / MT19937), plane stride `plane`
   size_t plane;
   const double* eps;
   double* stats;
   int* stop_iter;
   const spgg_rep_params* params;
   int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
+  int PB;                 // border-record slots per tile (pub_slots)
 };
 
 // What a step launch needs to pick and size the kernel instance.
 struct LaunchCfg {
-  int m2, as, rq, rng, tw, total_tiles;
+  int m2, as, rq, rng, twc, total_tiles;
   size_t lds_bytes;
 };
 
@@ -90,8 +92,34 @@ struct LaunchCfg {
 template <int ALG>
 void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s);
 
-// Agents per thread of operator ALG's kernel (Double-Q holds two tables in registers).
-constexpr int apt_of(int alg) { return alg == SPGG_ALG_DOUBLE_Q ? 2 : 4; }
+// Agents per thread of operator ALG's kernel: tiles of up to 1024 agents
+// (Double-Q, holding two tables in registers: 512).
+constexpr int apt_of(int alg) { return (alg == SPGG_ALG_DOUBLE_Q ? 512 : 1024) / kBlock; }
+// Per-thread register windows of the flattened staging walk (S / R halos of a
+// tile of <= 1024 agents; host-checked).
+constexpr int js_of(bool m2) { return kBlock == 256 ? (m2 ? 8 : 7) : 4; }
+constexpr int jr_of() { return kBlock == 256 ? 6 : 3; }
+// Doubles per agent in Q and fields per border record (Double-Q: both tables).
+constexpr int qw_of(int alg) { return alg == SPGG_ALG_DOUBLE_Q ? 8 : 4; }
+constexpr int pf_of(int alg) { return alg == SPGG_ALG_DOUBLE_Q ? 5 : 3; }
+
+// Border records.  An agent within HA cells of its tile's edge is read by the
+// ring recompute of a neighbouring tile (every ring cell of a tile is a border
+// cell of its owner, for any tiling and wrap).  Slots of a th x tw tile: the
+// HA top rows, the HA bottom rows, then HA left + HA right cells of each
+// middle row (row-major within each part, so tile edges read coalesced).
+__host__ __device__ inline int pub_slots(int TW, int TH, int HA) {
+  return 2 * HA * TW + (TH > 2 * HA ? (TH - 2 * HA) * 2 * HA : 0);
+}
+__host__ __device__ inline bool is_border(int r, int c, int th, int tw, int HA) {
+  return r < HA || r >= th - HA || c < HA || c >= tw - HA;
+}
+__host__ __device__ inline int border_slot(int r, int c, int th, int tw, int HA) {
+  if (r < HA) return r * tw + c;
+  if (r >= th - HA) return (r - th + 2 * HA) * tw + c;
+  const int cc = c < HA ? c : c - tw + 2 * HA;
+  return 2 * HA * tw + (r - HA) * 2 * HA + cc;
+}
 
 }  // namespace spgg_impl
 
@@ -103,22 +131,23 @@ constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
 
 
 struct LdsLayout {
-  int sw, sh, rw, rh, aw, ah;
-  int off_R, off_Rn, off_Rew, off_S, off_A, bytes;
+  int sw, sh, aw, ah;
+  int off_Rew, off_R, off_Rn, off_S, off_A, bytes;
 };
 
 // 16-byte aligned carve: f64 first, then the R planes (rsz = 8 or 1), then bytes.
-__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HR, int HA, int rsz) {
+// S planes: tile + halo HS (payoffs over tile + HA); everything else tile + HA.
+__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, int rsz) {
   LdsLayout l;
   l.sw = tw + 2 * HS; l.sh = th + 2 * HS;
-  l.rw = tw + 2 * HR; l.rh = th + 2 * HR;
   l.aw = tw + 2 * HA; l.ah = th + 2 * HA;
+  const int na = l.aw * l.ah;
   int off = (12 + kWaves * 64) * 8;  // payoff table + reduction scratch
-  l.off_Rew = off; off += ((l.aw * l.ah * 8 + 15) / 16) * 16;
-  l.off_R = off;   off += ((l.rw * l.rh * rsz + 15) / 16) * 16;
-  l.off_Rn = off;  off += ((l.aw * l.ah * rsz + 15) / 16) * 16;
-  l.off_S = off;   off += ((l.sw * l.sh + 15) / 16) * 16;
-  l.off_A = off;   off += ((l.aw * l.ah + 15) / 16) * 16;
+  l.off_Rew = off;  off += ((na * 8 + 15) / 16) * 16;
+  l.off_R = off;    off += ((na * rsz + 15) / 16) * 16;
+  l.off_Rn = off;   off += ((na * rsz + 15) / 16) * 16;
+  l.off_S = off;    off += ((l.sw * l.sh + 15) / 16) * 16;
+  l.off_A = off;    off += ((na + 15) / 16) * 16;
   l.bytes = off;
   return l;
 }
@@ -188,22 +217,24 @@ __device__ __forceinline__ int rep_state_lds(const double* R, int c, int w) {
   return acc >= rep_threshold(M2) ? 1 : 0;
 }
 
-// Deferred NI of iteration t-1 on one agent's Q (spgg.py:489-509).
-__device__ __forceinline__ double apply_pending(double (&q)[4], uint8_t b, double md, double kappa,
-                                                double lam_den, double lam_rcp) {
-  const int e = ((b >> 1) & 1) * 2 + (b & 1);  // (s_old, a) of iteration t-1
+// The deferred NI term nu of iteration t-1 (spgg.py:489-509): lambda times
+// +-1 by whether the best neighbour's action matched (S_t bit 2).
+__device__ __forceinline__ double pending_nu(uint8_t b, double md, double kappa, double lam_den, double lam_rcp) {
   const double lam = div_uniform(kappa * md, lam_den, lam_rcp);  // (kappa*max(0,md))/(gmax+eps)
-  const double nu = lam * (((b >> 2) & 1) ? 1.0 : -1.0);
-  q_set(q, e, q_get(q, e) + nu);
-  return nu;
+  return lam * (((b >> 2) & 1) ? 1.0 : -1.0);
 }
 
-template <int K>
-__device__ __forceinline__ void wave_partials(double (&v)[K], double* red, int base) {
-  transpose_level<K, 32, K>(v, threadIdx.x & 63);
+// (s_old, a) entry index of iteration t-1 recorded in S_t bits 0-1.
+__device__ __forceinline__ int pending_entry(uint8_t b) { return ((b >> 1) & 1) * 2 + (b & 1); }
+
+// Wave sums of K values into red[wave*64 + base + k] (f64, or packed integer
+// counters stored as exact doubles).
+template <int K, typename T>
+__device__ __forceinline__ void wave_partials(T (&v)[K], double* red, int base) {
+  transpose_level<K, 32, K, T>(v, threadIdx.x & 63);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int per = 64 / K;
-  if ((lane & (per - 1)) == 0) red[wave * 64 + base + lane / per] = v[0];
+  if ((lane & (per - 1)) == 0) red[wave * 64 + base + lane / per] = (double)v[0];
 }
 
 // Periodic index for x in [-L, 2L) (every halo offset here is <= 4 < L
@@ -245,6 +276,44 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
     if (tid + j * kBlock < total) dst[di[j]] = buf[j];
 }
 
+// Row-per-wave variant for a compile-time window width W <= 64 (TWC kernels,
+// L >= 2W): wave w copies rows w, w+4, ...; the row index and its wrap are
+// wave-uniform (scalar ALU), the column wrap is computed once per lane, so a
+// row costs ~3 vector instructions instead of ~30 for the flattened walk.
+template <int J, int W, int PITCH, typename T>
+__device__ __forceinline__ void stage_rows(T* dst, const T* src, int h, int y0, int x0, int L) {
+  static_assert(W <= 64, "one row per wave instruction");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int gx = x0 + lane;
+  gx += gx < 0 ? L : 0;
+  gx -= gx >= L ? L : 0;
+  const bool in_row = lane < W;
+  T buf[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int row = wave + j * kWaves;
+    int gy = y0 + row;
+    gy += gy < 0 ? L : 0;
+    gy -= gy >= L ? L : 0;
+    if (in_row && row < h) buf[j] = src[gy * L + gx];
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int row = wave + j * kWaves;
+    if (in_row && row < h) dst[row * PITCH + lane] = buf[j];
+  }
+}
+
+// Stage an h x w window: row-per-wave when the width is a compile-time
+// constant (TWC), else the flattened walk.
+template <int TWC, int HALO, int JF, int JR, typename T>
+__device__ __forceinline__ void stage(T* dst, int pitch, const T* src, int h, int w, int y0, int x0, int L,
+                                      bool tiny) {
+  if constexpr (TWC > 0) stage_rows<JR, TWC + 2 * HALO, TWC + 2 * HALO>(dst, src, h, y0, x0, L);
+  else stage_region<JF>(dst, pitch, src, h, w, y0, x0, L, tiny);
+}
+
 // 1/x to full f64 precision for DIAGNOSTIC quotients only (history values,
 // tolerance 1e-5): hardware estimate + two Newton steps, no IEEE division.
 __device__ __forceinline__ double rcp_diag(double x) {
@@ -254,9 +323,10 @@ __device__ __forceinline__ double rcp_diag(double x) {
   return r;
 }
 
-// Packed 8-bit per-thread counters (a thread owns <= 4 agents).
-enum { C_SWCD = 0, C_SWDC = 8, C_NCOOP1 = 16, C_NMD = 24 };   // cnt0
-enum { C_NMD2 = 0, C_GC0 = 8 };                                // cnt1: GC0..2 at 8,16,24; cnt2: GC3..5
+// History counters as 16-bit fields f = 0..10, two per dword (word f>>1,
+// half f&1; a workgroup counts at most 1024 agents, so fields never carry):
+//   SW_CD, SW_DC, NCOOP, NMD_POS, NMD_POS2, GC0, GC1, ..., GC5.
+// Words 2-3 and 4-5 are accumulated as 64-bit pairs (fields 4-7, 8-11).
 
 // Q table helpers.  QB = 1 for Double Q-learning (second table qb), else the
 // qb arrays are dead and the compiler drops them.
@@ -348,6 +418,27 @@ __device__ __forceinline__ void select_row(const double (&q)[4], const double (&
   }
 }
 
+// Diagnostic TD on the UPDATED table (spgg.py:446-473) for every operator but
+// SARSA (whose diagnostic target is a fresh eps-greedy draw): |diag_alpha*td'|
+// with e = (s_old, a) and sn the new state.  Used right after the TD update
+// and again, on the same stored table, when the next launch recomputes it.
+template <int ALG>
+__device__ __forceinline__ float diag_td(const double (&q)[4], const double (&qb)[ALG == ALG_DQ ? 4 : 1], int e,
+                                         int sn, double rew, const spgg_rep_params& pg, double eps) {
+  double td2;
+  if constexpr (ALG == ALG_DQ) {  // on the mean table (spgg.py:463-467)
+    const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
+    const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
+    const double m0 = sn ? m10 : m00, m1 = sn ? m11 : m01;
+    td2 = (rew + pg.diag_gamma * fmax(m0, m1)) - mean2(q_get(q, e), q_get(qb, e));
+  } else {
+    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];
+    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps) : fmax(w0, w1);
+    td2 = (rew + pg.diag_gamma * target2) - q_get(q, e);
+  }
+  return (float)fabs(pg.diag_alpha * td2);
+}
+
 // TD update of the operator for one agent (algorithms.py:112-341) and the
 // diagnostic TD on the updated table (spgg.py:446-473).  Returns |diag_alpha*td'|.
 template <int ALG, int RNG>
@@ -356,7 +447,6 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const spgg_rep_par
                                            double (&q)[4], double (&qb)[ALG == ALG_DQ ? 4 : 1]) {
   const double alpha = pg.alpha, gamma = pg.gamma, dgamma = pg.diag_gamma;
   const int e = so * 2 + act;
-  double td2;
   if constexpr (ALG == ALG_DQ) {
     // scalar copies: value selects only (pointer selects into the tables
     // would keep them out of registers)
@@ -374,11 +464,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const spgg_rep_par
     const double nq1 = up1 ? u1 : qc1, nq2 = up1 ? qc2 : u2;
     q[0] = e == 0 ? nq1 : x0; q[1] = e == 1 ? nq1 : x1; q[2] = e == 2 ? nq1 : x2; q[3] = e == 3 ? nq1 : x3;
     qb[0] = e == 0 ? nq2 : y0; qb[1] = e == 1 ? nq2 : y1; qb[2] = e == 2 ? nq2 : y2; qb[3] = e == 3 ? nq2 : y3;
-    // diagnostic on the mean table (spgg.py:463-467)
-    const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
-    const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
-    const double m0 = sn ? m10 : m00, m1 = sn ? m11 : m01;
-    td2 = (rew + dgamma * fmax(m0, m1)) - mean2(nq1, nq2);
+    return diag_td<ALG>(q, qb, e, sn, rew, pg, eps);
   } else {
     const double qc = q_get(q, e);
     const double v0 = sn ? q[2] : q[0], v1 = sn ? q[3] : q[1];
@@ -395,31 +481,40 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const spgg_rep_par
     const double td = (rew + gamma * target) - qc;
     const double q1 = qc + alpha * td;
     q_set(q, e, q1);
-    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];       // updated table
-    double target2;
     if constexpr (ALG == ALG_SARSA) {
+      const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];     // updated table
       int ex, rbt;                                                   // diagnostic select, spgg.py:452
       draw_pair<RNG>(a, rb, g, t, key, eps, 2, &ex, &rbt);
-      target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
-    } else if constexpr (ALG == ALG_ES) {
-      target2 = expected_q(w0, w1, eps);
+      const double target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
+      return (float)fabs(pg.diag_alpha * ((rew + dgamma * target2) - q1));
     } else {
-      target2 = fmax(w0, w1);
+      return diag_td<ALG>(q, qb, e, sn, rew, pg, eps);
     }
-    td2 = (rew + dgamma * target2) - q1;
   }
-  return (float)fabs(pg.diag_alpha * td2);
 }
 
-// TWC > 0: compile-time tile width (LDS row pitches become immediates in every
-// stencil address); TWC = 0: run-time width.
+// ONE launch = iteration t of every replica (or, fin_only, the final deferred
+// NI term).  TWC > 0: compile-time tile width, every tile full width (host:
+// L % TWC == 0), so LDS pitches and region divisions are immediates.
+//
+// Buffers: S and R ping-pong by parity (neighbours read their halos while the
+// owner writes the next ones); Q, max_diff and |alpha*td'| IN PLACE (an
+// agent's entries are read and written only by its owner; the ring recompute
+// reads the owner's border record instead), border records ping-pong.  Per
+// agent-step HBM/Infinity-Cache traffic: Q 32 B read + 32 B written, md 8 + 8,
+// atd 4 + 4, S/R ~5 B, border records ~6 B; the working set of cfg3 (~235 MB)
+// stays within the 256 MB Infinity Cache (a ping-ponged Q alone was 270 MB).
 template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
-__global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
+// Occupancy floor (waves per SIMD), build knob for A/B timing.
+#ifndef SPGG_MIN_WAVES
+#define SPGG_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
   using RT = RStore<RQ>;
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
-  constexpr int HR = 2 * HA;      // R_t halo: states of ring agents
-  constexpr int HS = HA + 2;      // S_t halo: payoffs of ring agents
+  constexpr int HS = HA + 2;      // S halo: payoffs over tile + HA
   constexpr int QB = ALG == ALG_DQ ? 1 : 0;
+  constexpr int PF = spgg_impl::pf_of(ALG);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -435,21 +530,21 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   if (SPGG_ABLATE & 64) return;
 
   const int L = a.L, n = a.n;
-  const bool tiny = L < 8;
+  const bool tiny = TWC ? false : L < 8;  // TWC => L % TWC == 0
   const int tyi = tile / a.tiles_x, txi = tile - (tile / a.tiles_x) * a.tiles_x;
   const int y0 = tyi * a.TH, x0 = txi * a.TW;
-  const int th = min(a.TH, L - y0), tw = min(a.TW, L - x0);
+  const int th = min(a.TH, L - y0), tw = TWC ? TWC : min(a.TW, L - x0);
   // LDS pitches from the full tile width (constants when TWC > 0); edge tiles
   // use the top-left part of each region
-  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HR, HA, (int)sizeof(RT))
-                           : lds_layout(tw, th, HS, HR, HA, (int)sizeof(RT));
+  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HA, (int)sizeof(RT))
+                           : lds_layout(tw, th, HS, HA, (int)sizeof(RT));
   double* tab = reinterpret_cast<double*>(smem);
   double* red = tab + 12;
+  double* sRew = reinterpret_cast<double*>(smem + ly.off_Rew);
   RT* sR = reinterpret_cast<RT*>(smem + ly.off_R);
   RT* sRn = reinterpret_cast<RT*>(smem + ly.off_Rn);
   const RT* Rin = reinterpret_cast<const RT*>(a.R_in);
   RT* Rout = reinterpret_cast<RT*>(a.R_out);
-  double* sRew = reinterpret_cast<double*>(smem + ly.off_Rew);
   uint8_t* sS = smem + ly.off_S;
   uint8_t* sA = smem + ly.off_A;
 
@@ -472,6 +567,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
   const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
                         (uint32_t)pg.stream_id * 0xC2B2AE35u;
+  const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
 
   // ---- phase 0: owned-agent registers + LDS staging ----------------------
   // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
@@ -495,9 +591,9 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       if constexpr (QB) qb[u][0] = qb[u][1] = qb[u][2] = qb[u][3] = 0.0;
       if (k < n_own) {
         gidx[u] = (y0 + r) * L + (x0 + c);
-        load_q<QB>(a.Q_in, rb + gidx[u], q[u], qb[u]);
+        load_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
         if (pending) {
-          md_own[u] = a.md_in[rb + gidx[u]];
+          md_own[u] = a.md[rb + gidx[u]];
           atd_own[u] = a.atd[rb + gidx[u]];
         }
       }
@@ -510,9 +606,26 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     }
   }
   if (tid < 12) tab[tid] = tid < 6 ? pg.pay_c[tid] : pg.pay_d[tid - 6];
-  stage_region<(M2 ? 8 : 7)>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny);
-  if (!AS && !fin_only)
-    stage_region<(M2 ? 8 : 6)>(sR, ly.rw, Rin + rb, th + 2 * HR, tw + 2 * HR, y0 - HR, x0 - HR, L, tiny);
+  // row-per-wave windows (TWC): rows <= TH + 2*halo with TH <= 25 (host-checked)
+  constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
+  constexpr int JSF = spgg_impl::js_of(M2), JRF = spgg_impl::jr_of();
+  stage<TWC, HS, JSF, JSR>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny);
+  if (!AS) stage<TWC, HA, JRF, JRR>(sR, ly.aw, Rin + rb, ah, aw, y0 - HA, x0 - HA, L, tiny);
+  __syncthreads();
+  if (SPGG_ABLATE & 128) {  // memory floor: write back what was read
+#pragma unroll
+    for (int u = 0; u < APT; ++u) {
+      if (gidx[u] < 0) continue;
+      const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+      store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
+      a.md[rb + gidx[u]] = md_own[u];
+      a.atd[rb + gidx[u]] = atd_own[u];
+      a.S_out[rb + gidx[u]] = sS[(r + HS) * ly.sw + (c + HS)];
+      if (!AS) Rout[rb + gidx[u]] = sR[(r + HA) * ly.aw + (c + HA)];
+    }
+    return;
+  }
+
   __syncthreads();
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
@@ -527,19 +640,19 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         if (gidx[u] < 0) continue;
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
-        const double nu = apply_pending(q[u], b, md_own[u], kappa, lam_den, lam_rcp);
-        if constexpr (QB) {  // both tables (spgg.py:496-502)
-          const int e = ((b >> 1) & 1) * 2 + (b & 1);
-          q_set(qb[u], e, q_get(qb[u], e) + nu);
-        }
+        const int e = pending_entry(b);
+        const float atd = atd_own[u];
+        const double nu = pending_nu(b, md_own[u], kappa, lam_den, lam_rcp);
+        q_set(q[u], e, q_get(q[u], e) + nu);
+        if constexpr (QB) q_set(qb[u], e, q_get(qb[u], e) + nu);  // both tables (spgg.py:496-502)
         const double anu = fabs(nu);
-        v[0] += (anu * rcp_diag(((double)atd_own[u] + anu) + 1e-8)) * 100.0;  // spgg.py:512
-        const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                        // prev_S of t-1 == C
+        v[0] += (anu * rcp_diag(((double)atd + anu) + 1e-8)) * 100.0;  // spgg.py:512
+        const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                  // prev_S of t-1 == C
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {                                          // spgg.py:562-583
-          const double qv = QB ? mean2(q[u][e], qb[u][QB ? e : 0]) : q[u][e];
-          v[1 + e] += qv;
-          v[5 + e] += qv * cm;
+        for (int e2 = 0; e2 < 4; ++e2) {                                 // spgg.py:562-583
+          const double qv = QB ? mean2(q[u][e2], qb[u][QB ? e2 : 0]) : q[u][e2];
+          v[1 + e2] += qv;
+          v[5 + e2] += qv * cm;
         }
       }
     }
@@ -549,7 +662,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       if (gidx[u] < 0) continue;
-      store_q<QB>(a.Q_out, rb + gidx[u], q[u], qb[u]);
+      store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
     }
   }
 
@@ -559,7 +672,8 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   double va[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) va[k] = 0.0;
-  unsigned cnt0 = 0, cnt1 = 0, cnt2 = 0;
+  uint32_t cw0 = 0, cw1 = 0;
+  uint64_t cwa = 0, cwb = 0;
   int own_bits[APT];  // a | so<<1 | s_t<<3
 #pragma unroll
   for (int u = 0; u < APT; ++u) {
@@ -567,9 +681,10 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     if (fin_only || gidx[u] < 0) continue;
     const int r = rc[u] >> 16, c = rc[u] & 0xffff;
     const int cs = (r + HS) * ly.sw + (c + HS);
+    const int ca = (r + HA) * ly.aw + (c + HA);
     const int s_t = sS[cs] & 1;
     const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
-    const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[(r + HR) * ly.rw + (c + HR)];
+    const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[ca];
     const double cmask = s_t ? 0.0 : 1.0;
     va[0] += P;                                           // spgg.py:388-390
     va[1] += P * cmask;
@@ -577,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     if (!acting) continue;
     int so;                                               // spgg.py:409
     if constexpr (AS) so = s_t == 0 ? 1 : 0;
-    else so = rep_state_lds<M2>(sR, (r + HR) * ly.rw + (c + HR), ly.rw);
+    else so = rep_state_lds<M2>(sR, ca, ly.aw);
     int ex, rbt;                                          // algorithms.py:105-109
     draw_pair<RNG>(a, rb, gidx[u], t, pkey, eps_t, 0, &ex, &rbt);
     double qs0, qs1;
@@ -587,15 +702,14 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
     const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
     const double wpp = w_p * P, wrr = w_rep * rr;
     const double rew = wpp + wrr;
-    const int ca = (r + HA) * ly.aw + (c + HA);
     sA[ca] = (uint8_t)act;
     sRn[ca] = (RT)rn;
     sRew[ca] = rew;
     Rout[rb + gidx[u]] = (RT)rn;
     own_bits[u] = act | (so << 1) | (s_t << 3);
-    cnt0 += ((s_t == 0 && act == 1) ? 1u : 0u) << C_SWCD;  // spgg.py:419-420
-    cnt0 += ((s_t == 1 && act == 0) ? 1u : 0u) << C_SWDC;
-    cnt0 += (act == 0 ? 1u : 0u) << C_NCOOP1;
+    cw0 += (s_t == 0 && act == 1) ? 1u : 0u;             // spgg.py:419-420
+    cw0 += (s_t == 1 && act == 0) ? 0x10000u : 0u;
+    cw1 += act == 0 ? 1u : 0u;
     va[3] += wpp;                                         // spgg.py:425-426
     va[4] += wrr;
     va[5] += rew;                                         // spgg.py:529-545
@@ -605,10 +719,13 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   }
 
   // ---- phase 1c: recompute the ring of neighbours (distance <= M) --------
+  // Their Q row of state s_t (S_t bit 4) and max_diff come from the owner's
+  // border record of iteration t-1; the owner applies the same NI term to
+  // the same entry, so both agree bit for bit.
   if (acting && !(SPGG_ABLATE & 4)) {
-    const int aw = tw + 2 * HA;  // ring enumeration over the actual tile
     const int band = HA * aw;
-    const int ring = aw * (th + 2 * HA) - n_own;
+    const int ring = aw * ah - n_own;
+    const double* pin = a.pub_in + (size_t)rep * a.tiles_per_rep * PF * a.PB;
     for (int k = tid; k < ring; k += kBlock) {
       int ay, ax;
       if (k < band) {
@@ -624,41 +741,43 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         const int cc = k3 - (k3 / (2 * HA)) * (2 * HA);
         ax = cc < HA ? cc : tw + cc;
       }
-      const int g = wrap1(y0 - HA + ay, L, tiny) * L + wrap1(x0 - HA + ax, L, tiny);
+      const int gy = wrap1(y0 - HA + ay, L, tiny), gx = wrap1(x0 - HA + ax, L, tiny);
+      const int g = gy * L + gx;
+      // owner tile and border slot
+      const int oty = gy / a.TH, otx = gx / a.TW;
+      const int orr = gy - oty * a.TH, occ = gx - otx * a.TW;
+      const int oth = min(a.TH, L - oty * a.TH), otw = min(a.TW, L - otx * a.TW);
+      const double* rec = pin + (size_t)(oty * a.tiles_x + otx) * PF * a.PB +
+                          spgg_impl::border_slot(orr, occ, oth, otw, HA);
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
       const uint8_t b = sS[cs];
-      const int s_t = b & 1;
-      double qq[4], qqb[QB ? 4 : 1];
-      load_q<QB>(a.Q_in, rb + g, qq, qqb);
+      double v0 = rec[0], v1 = rec[a.PB], w0 = 0.0, w1 = 0.0;
+      if constexpr (QB) {
+        w0 = rec[2 * a.PB];
+        w1 = rec[3 * a.PB];
+      }
       if (pending) {
-        const double nu = apply_pending(qq, b, a.md_in[rb + g], kappa, lam_den, lam_rcp);
-        if constexpr (QB) {
-          const int e = ((b >> 1) & 1) * 2 + (b & 1);
-          q_set(qqb, e, q_get(qqb, e) + nu);
+        const int e = pending_entry(b);
+        if ((e >> 1) == ((b >> 4) & 1)) {  // the NI entry lies in the published row
+          const double nu = pending_nu(b, rec[(PF - 1) * a.PB], kappa, lam_den, lam_rcp);
+          if (e & 1) v1 = v1 + nu; else v0 = v0 + nu;
+          if constexpr (QB) {
+            if (e & 1) w1 = w1 + nu; else w0 = w0 + nu;
+          }
         }
       }
       const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
-      int so;
-      RVal<RQ> r_t;
-      if constexpr (AS) {
-        so = s_t == 0 ? 1 : 0;
-        r_t = 0;  // R of ring agents is not needed in action-state mode
-      } else {
-        const int cr = (ay + (HR - HA)) * ly.rw + (ax + (HR - HA));
-        so = rep_state_lds<M2>(sR, cr, ly.rw);
-        r_t = sR[cr];
-      }
+      const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sR[ay * ly.aw + ax]);
       int ex, rbt;
       draw_pair<RNG>(a, rb, g, t, pkey, eps_t, 0, &ex, &rbt);
-      double qs0, qs1;
-      select_row<QB>(qq, qqb, so, &qs0, &qs1);
-      const int act = ex ? rbt : greedy2(qs0, qs1);
+      const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
       const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
-      const double rew = w_p * P + w_rep * (act == 0 ? 0.5 : 0.0);
+      const double rr = act == 0 ? 0.5 : 0.0;
+      const double wpp = w_p * P, wrr = w_rep * rr;
       const int ca = ay * ly.aw + ax;
       sA[ca] = (uint8_t)act;
       sRn[ca] = (RT)rn;
-      sRew[ca] = rew;
+      sRew[ca] = wpp + wrr;
     }
   }
   __syncthreads();
@@ -666,6 +785,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;
   if (acting) {
+    double* pout = a.pub_out + (size_t)(rep * a.tiles_per_rep + tile) * PF * a.PB;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       if (gidx[u] < 0) continue;
@@ -676,8 +796,9 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      a.atd[rb + gidx[u]] = td_update<ALG, RNG>(a, pg, rb, gidx[u], t, pkey, eps_t, rew, so, act, sn, q[u], qb[u]);
-      store_q<QB>(a.Q_out, rb + gidx[u], q[u], qb[u]);
+      const float atd = td_update<ALG, RNG>(a, pg, rb, gidx[u], t, pkey, eps_t, rew, so, act, sn, q[u], qb[u]);
+      a.atd[rb + gidx[u]] = atd;
+      store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -697,37 +818,33 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       }
       const int dp = sA[sel] == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
-      a.md_out[rb + gidx[u]] = mdp;
       bmax = fmax(bmax, mdp);
-      a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2));
+      a.md[rb + gidx[u]] = mdp;
+      a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
+      if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
+        double* rec = pout + spgg_impl::border_slot(r, c, th, tw, HA);
+        rec[0] = sn ? q[u][2] : q[u][0];
+        rec[a.PB] = sn ? q[u][3] : q[u][1];
+        if constexpr (QB) {
+          rec[2 * a.PB] = sn ? qb[u][QB ? 2 : 0] : qb[u][0];
+          rec[3 * a.PB] = sn ? qb[u][QB ? 3 : 0] : qb[u][QB ? 1 : 0];
+        }
+        rec[(PF - 1) * a.PB] = mdp;
+      }
       // group composition on S_{t+1}, spgg.py:585-592
       const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
-      if (nd < 3) cnt1 += 1u << (C_GC0 + 8 * nd);
-      else cnt2 += 1u << (8 * (nd - 3));
+      if (nd < 3) cwa += 1ull << (16 * (nd + 1));          // GC0..2: fields 5-7
+      else cwb += 1ull << (16 * (nd - 3));                  // GC3..5: fields 8-10
       if (md > 0.0) {                                       // spgg.py:520-523
-        cnt0 += 1u << C_NMD;
-        if (ks >= 4) cnt1 += 1u << C_NMD2;
+        cw1 += 0x10000u;
+        if (ks >= 4) cwa += 1u;
       }
     }
   }
-  {  // slot layout in red[wave*64 + 16 ..]: va[0..7], then 11 counts
-    double v[32];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = va[k];
-    v[8] = (double)((cnt0 >> C_SWCD) & 0xff);
-    v[9] = (double)((cnt0 >> C_SWDC) & 0xff);
-    v[10] = (double)((cnt0 >> C_NCOOP1) & 0xff);
-    v[11] = (double)((cnt0 >> C_NMD) & 0xff);
-    v[12] = (double)((cnt1 >> C_NMD2) & 0xff);
-    v[13] = (double)((cnt1 >> 8) & 0xff);
-    v[14] = (double)((cnt1 >> 16) & 0xff);
-    v[15] = (double)((cnt1 >> 24) & 0xff);
-    v[16] = (double)(cnt2 & 0xff);
-    v[17] = (double)((cnt2 >> 8) & 0xff);
-    v[18] = (double)((cnt2 >> 16) & 0xff);
-#pragma unroll
-    for (int k = 19; k < 32; ++k) v[k] = 0.0;
-    if (!(SPGG_ABLATE & 8)) wave_partials<32>(v, red, 16);
+  if (!(SPGG_ABLATE & 8)) {  // red[wave*64 + 16..23]: va[0..7]; 24..29: counter words
+    wave_partials<8>(va, red, 16);
+    uint32_t cw[8] = {cw0, cw1, (uint32_t)cwa, (uint32_t)(cwa >> 32), (uint32_t)cwb, (uint32_t)(cwb >> 32), 0u, 0u};
+    wave_partials<8>(cw, red, 24);
   }
   __syncthreads();
 
@@ -746,7 +863,7 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
         else { k = SPGG_ST_SUMQ_D + tid - 9; src = tid - 8; src_c = tid - 4; }
       }
     } else if (tid >= 16 && tid < 16 + 22 && !fin_only) {
-      const int j = tid - 16;
+      const int j = tid - 16;  // 0-7 va, 8-18 counters, 19-20 derived
       static constexpr int kmap[22] = {
           SPGG_ST_SUMP, SPGG_ST_SUMP_C, SPGG_ST_SUMR, SPGG_ST_SUM_WPP, SPGG_ST_SUM_WRR,
           -1 /* reward total: only feeds REW_D */, SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C,
@@ -761,12 +878,16 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
       if (k >= 0 && (acting || start_val)) slot = (j == 10) ? t + 1 : t;
     }
     if (slot >= 0) {
+      const int j = tid - 16;
+      const bool counter = j >= 8 && j <= 18;
+      const int word = 24 + ((j - 8) >> 1);
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) {
-        tot[0] += red[w * 64 + src];
+        tot[0] += red[w * 64 + (counter ? word : src)];
         if (src_c >= 0) tot[1] += red[w * 64 + src_c];
       }
       double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
+      if (counter) val = (double)(((unsigned long long)tot[0] >> (16 * ((j - 8) & 1))) & 0xffffu);
       if (RQ && k == SPGG_ST_SUMR) val *= pg.rep_unit;
       if (val != 0.0 && (!(SPGG_ABLATE & 2) || k == SPGG_ST_NCOOP))
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);
@@ -783,6 +904,65 @@ __global__ __launch_bounds__(kBlock) void spgg_step_kernel(TileArgs a, int t, in
   }
 }
 
+// Prologue of iteration 1: state s_1 of every agent into S_1 bit 4 and the
+// border records of the initial table (row s_1; no pending NI), so launch 1's
+// ring recompute reads the same records as every later launch.
+template <bool M2, bool AS, bool RQ, int ALG>
+__global__ __launch_bounds__(kBlock) void spgg_publish_init_kernel(TileArgs a) {
+  using RT = RStore<RQ>;
+  constexpr int HA = M2 ? 2 : 1;
+  constexpr int QB = ALG == ALG_DQ ? 1 : 0;
+  constexpr int PF = spgg_impl::pf_of(ALG);
+  const int rep = blockIdx.y;
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= a.n) return;
+  const int L = a.L;
+  const int y = g / L, x = g - (g / L) * L;
+  const size_t rb = (size_t)rep * a.n;
+  uint8_t* S = a.S_out;  // S_1, updated in place
+  int s1;
+  if constexpr (AS) {
+    s1 = (S[rb + g] & 1) ? 0 : 1;
+  } else {  // spgg.py:296-307 over R_1, offsets in the reference's order
+    const RT* R = reinterpret_cast<const RT*>(a.R_in) + rb;
+    const int ym = wrap(y - 1, L), yp = wrap(y + 1, L), xm = wrap(x - 1, L), xp = wrap(x + 1, L);
+    RT cell[13];
+    cell[0] = R[y * L + x]; cell[1] = R[ym * L + x]; cell[2] = R[yp * L + x];
+    cell[3] = R[y * L + xm]; cell[4] = R[y * L + xp];
+    int nc = 5;
+    if constexpr (M2) {
+      const int yM = wrap(y - 2, L), yP = wrap(y + 2, L), xM = wrap(x - 2, L), xP = wrap(x + 2, L);
+      cell[5] = R[yM * L + x]; cell[6] = R[yP * L + x]; cell[7] = R[y * L + xM]; cell[8] = R[y * L + xP];
+      cell[9] = R[ym * L + xm]; cell[10] = R[ym * L + xp]; cell[11] = R[yp * L + xm]; cell[12] = R[yp * L + xp];
+      nc = 13;
+    }
+    if constexpr (RQ) {
+      int acc = 0;
+      for (int i = 0; i < nc; ++i) acc += cell[i];
+      s1 = acc > 0 ? 1 : 0;
+    } else {
+      double acc = 0.0;
+      for (int i = 0; i < nc; ++i) acc += cell[i];
+      s1 = acc >= rep_threshold(M2) ? 1 : 0;
+    }
+  }
+  S[rb + g] = (uint8_t)((S[rb + g] & 0x0f) | (s1 << 4));
+  const int ty = y / a.TH, tx = x / a.TW;
+  const int r = y - ty * a.TH, c = x - tx * a.TW;
+  const int th = min(a.TH, L - ty * a.TH), tw = min(a.TW, L - tx * a.TW);
+  if (!spgg_impl::is_border(r, c, th, tw, HA)) return;
+  const double* Q = a.Q + (rb + g) * (QB ? 8 : 4);
+  double* rec = a.pub_out + (size_t)(rep * a.tiles_per_rep + ty * a.tiles_x + tx) * PF * a.PB +
+                spgg_impl::border_slot(r, c, th, tw, HA);
+  rec[0] = Q[2 * s1];
+  rec[a.PB] = Q[2 * s1 + 1];
+  if constexpr (QB) {
+    rec[2 * a.PB] = Q[4 + 2 * s1];
+    rec[3 * a.PB] = Q[4 + 2 * s1 + 1];
+  }
+  rec[(PF - 1) * a.PB] = 0.0;
+}
+
 }  // namespace
 
 namespace spgg_impl {
@@ -792,7 +972,7 @@ void launch_t(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_
   constexpr int APT = apt_of(ALG);
   const dim3 grid(((lc.total_tiles + 7) / 8) * 8);
 #ifndef SPGG_NO_TWC
-  if (lc.tw == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
+  if (lc.twc == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
     hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, APT, 40, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
                        t, fin);
   else
@@ -803,6 +983,11 @@ void launch_t(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_
 
 template <bool M2, bool AS, bool RQ, int ALG>
 void launch_rng(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
+  if (t == 0) {  // prologue of iteration 1 (border records of the initial table)
+    const dim3 grid((a.n + kBlock - 1) / kBlock, a.n_rep);
+    hipLaunchKernelGGL((spgg_publish_init_kernel<M2, AS, RQ, ALG>), grid, dim3(kBlock), 0, s, a);
+    return;
+  }
   if (lc.rng == SPGG_RNG_PHILOX) launch_t<M2, AS, RQ, SPGG_RNG_PHILOX, ALG>(lc, a, t, fin, s);
   else launch_t<M2, AS, RQ, SPGG_RNG_MT19937, ALG>(lc, a, t, fin, s);  // INJECT reads the same planes
 }
@@ -991,7 +1176,7 @@ struct spgg_ctx {
   bool params_set = false;
   spgg_rep_params* d_params = nullptr;
   int n = 0;
-  int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4;
+  int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4, PB = 0;
   size_t lds_bytes = 0;
   std::string err;
 };
@@ -1032,13 +1217,23 @@ void choose_tile(int L, int max_agents, int* TW, int* TH) {
   *TH = best_h;
 }
 
+// Iteration t reads S_t, R_t, records [(t-1)&1] and writes [t&1]; Q, md,
+// atd in place.  t = 0 addresses the iteration-1 prologue (S_1 and R_1 in,
+// records [0] out).
 TileArgs make_args(const spgg_ctx* c, int t) {
   TileArgs a{};
-  const int cur = (t - 1) & 1, nxt = t & 1;
-  a.S_in = c->buf.S[cur];   a.S_out = c->buf.S[nxt];
-  a.R_in = c->buf.R[cur];   a.R_out = c->buf.R[nxt];
-  a.Q_in = c->buf.Q[cur];   a.Q_out = c->buf.Q[nxt];
-  a.md_in = c->buf.md[cur]; a.md_out = c->buf.md[nxt];
+  if (t == 0) {
+    a.S_out = c->buf.S[0];
+    a.R_in = c->buf.R[0];
+    a.pub_out = c->buf.pub[0];
+  } else {
+    const int cur = (t - 1) & 1, nxt = t & 1;
+    a.S_in = c->buf.S[cur];    a.S_out = c->buf.S[nxt];
+    a.R_in = c->buf.R[cur];    a.R_out = c->buf.R[nxt];
+    a.pub_in = c->buf.pub[cur];  a.pub_out = c->buf.pub[nxt];
+  }
+  a.Q = c->buf.Q;
+  a.md = c->buf.md;
   a.atd = c->buf.atd;
   a.draws = c->buf.draws;
   a.plane = (size_t)c->buf.draw_plane_stride;
@@ -1054,6 +1249,7 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   a.tiles_per_rep = c->tiles_per_rep;
   a.n_rep = c->cfg.n_rep;
   a.slots = c->cfg.iterations + 2;
+  a.PB = c->PB;
   return a;
 }
 
@@ -1064,7 +1260,9 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   lc.as = c->cfg.state_mode == SPGG_STATE_ACTION;
   lc.rq = c->cfg.rep_int8 != 0;
   lc.rng = c->cfg.rng_mode;
-  lc.tw = c->TW;
+  // compile-time-width kernels: every tile full width, L >= 2 * window width,
+  // window rows within the row-per-wave register budget (4 * JSR / JRR)
+  lc.twc = (c->TW == 40 && c->cfg.L % 40 == 0 && c->cfg.L >= 120 && c->TH <= 25) ? 40 : 0;
   lc.total_tiles = c->cfg.n_rep * c->tiles_per_rep;
   lc.lds_bytes = c->lds_bytes;
   switch (c->cfg.algorithm) {
@@ -1121,11 +1319,12 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->tiles_x = (cfg->L + c->TW - 1) / c->TW;
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
   const int HA = cfg->second_order ? 2 : 1;
-  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, 2 * HA, HA, cfg->rep_int8 ? 1 : 8);
+  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8);
   c->lds_bytes = (size_t)ly.bytes;
+  c->PB = spgg_impl::pub_slots(c->TW, c->TH, HA);
   // stage_region's per-thread register window must cover the S and R halos
-  const int js = cfg->second_order ? 8 : 7, jr = cfg->second_order ? 8 : 6;
-  if (c->lds_bytes > 160 * 1024 || ly.sw * ly.sh > js * kBlock || ly.rw * ly.rh > jr * kBlock) {
+  const int js = spgg_impl::js_of(cfg->second_order != 0), jr = spgg_impl::jr_of();
+  if (c->lds_bytes > 160 * 1024 || ly.sw * ly.sh > js * kBlock || ly.aw * ly.ah > jr * kBlock) {
     delete c;
     return SPGG_E_ARG;
   }
@@ -1156,17 +1355,17 @@ int spgg_set_params(spgg_ctx* c, const spgg_rep_params* params) {
 int spgg_bind(spgg_ctx* c, const spgg_buffers* b) {
   if (!c || !b) return fail(c, SPGG_E_ARG, "null argument");
   for (int i = 0; i < 2; ++i)
-    if (!b->S[i] || !b->R[i] || !b->Q[i] || !b->md[i])
-      return fail(c, SPGG_E_ARG, "spgg_bind: a ping-pong buffer is null");
-  if (!b->atd || !b->eps || !b->stats || !b->stop_iter)
+    if (!b->S[i] || !b->R[i] || !b->pub[i])
+      return fail(c, SPGG_E_ARG, "spgg_bind: an S / R / border-record buffer is null");
+  if (!b->Q || !b->md || !b->atd || !b->eps || !b->stats || !b->stop_iter)
     return fail(c, SPGG_E_ARG, "spgg_bind: a required buffer is null");
   if (c->cfg.rng_mode != SPGG_RNG_PHILOX &&
       (!b->draws || b->draw_plane_stride < (int64_t)c->cfg.n_rep * c->n))
     return fail(c, SPGG_E_ARG, "spgg_bind: draw planes (stride >= n_rep*n) required for INJECT/MT19937");
   if (c->cfg.rng_mode == SPGG_RNG_MT19937 && !b->mt_state)
     return fail(c, SPGG_E_ARG, "spgg_bind: mt_state required for MT19937");
-  if (((reinterpret_cast<uintptr_t>(b->Q[0]) | reinterpret_cast<uintptr_t>(b->Q[1])) & 15) != 0)
-    return fail(c, SPGG_E_ARG, "spgg_bind: Q buffers must be 16-byte aligned");
+  if ((reinterpret_cast<uintptr_t>(b->Q) & 15) != 0)
+    return fail(c, SPGG_E_ARG, "spgg_bind: the Q buffer must be 16-byte aligned");
   c->buf = *b;
   c->bound = true;
   return SPGG_OK;
@@ -1180,6 +1379,7 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
   if (c->cfg.rng_mode == SPGG_RNG_INJECT && n_steps > 1)
     return fail(c, SPGG_E_ARG, "spgg_step: INJECT mode steps one iteration per call");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
   for (int t = t0; t < t0 + n_steps; ++t) {
     if (c->cfg.rng_mode == SPGG_RNG_MT19937) launch_draw(c, t, s);
     launch_step(c, t, 0, s);
@@ -1212,6 +1412,12 @@ int spgg_payoff(spgg_ctx* c, int32_t t, double* out, void* stream) {
   hipLaunchKernelGGL(spgg_payoff_kernel, grid, dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                      c->buf.S[(t - 1) & 1], c->d_params, out, c->cfg.L, c->n);
   return hip_check(c, hipGetLastError(), "spgg_payoff launch");
+}
+
+int spgg_pub_doubles(const spgg_ctx* c, int64_t* per_rep) {
+  if (!c || !per_rep) return SPGG_E_ARG;
+  *per_rep = (int64_t)c->tiles_per_rep * spgg_impl::pf_of(c->cfg.algorithm) * c->PB;
+  return SPGG_OK;
 }
 
 int spgg_tile_shape(const spgg_ctx* c, int32_t* tw, int32_t* th) {

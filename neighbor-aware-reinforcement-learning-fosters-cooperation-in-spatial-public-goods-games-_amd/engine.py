@@ -227,9 +227,10 @@ class BatchEngine:
                          and os.environ.get("SPGG_REP_F64", "0") != "1")
         self.rep_units = np.array([u if u is not None else 1.0 for u in units])
         self.Rep = torch.zeros((2, R, n), dtype=torch.int8 if self.rep_int8 else f64, device=d)
-        self.Qb = torch.zeros((2, R, n, self.QW), dtype=f64, device=d)
-        self.Qb[0].copy_(torch.from_numpy(Q0))
-        self.md = torch.zeros((2, R, n), dtype=f64, device=d)
+        # Q updated in place (reference layout (L,L,2,2) per replica)
+        self.Qb = torch.from_numpy(np.ascontiguousarray(Q0)).to(d)
+        # pending NI record, in place: max(0, max_diff) and |alpha*td'| (diagnostic)
+        self.md = torch.zeros((R, n), dtype=f64, device=d)
         self.atd = torch.zeros((R, n), dtype=torch.float32, device=d)
         # draw planes of one iteration (device MT19937 / inject), spgg_abi.h
         self.n_planes = C.DRAW_PLANES[self.alg]
@@ -275,11 +276,15 @@ class BatchEngine:
             C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
             arr = (C.RepParams * (r1 - r0))(*params[r0:r1])
             C.check(self.lib.spgg_set_params(ctx, arr), ctx, "spgg_set_params")
+            if g == 0:   # border records: library-defined size per replica
+                per = ctypes.c_int64()
+                C.check(self.lib.spgg_pub_doubles(ctx, ctypes.byref(per)), ctx, "spgg_pub_doubles")
+                self.pub = torch.zeros((2, self.R, max(1, per.value)), dtype=torch.float64, device=self.dev)
             b = C.Buffers()   # the group's replica slice of every buffer
             for i in range(2):
                 b.S[i], b.R[i] = self.S[i][r0].data_ptr(), self.Rep[i][r0].data_ptr()
-                b.Q[i], b.md[i] = self.Qb[i][r0].data_ptr(), self.md[i][r0].data_ptr()
-            b.atd = self.atd[r0].data_ptr()
+                b.pub[i] = self.pub[i][r0].data_ptr()
+            b.Q, b.md, b.atd = self.Qb[r0].data_ptr(), self.md[r0].data_ptr(), self.atd[r0].data_ptr()
             b.draws = self.draws[0, min(r0, self.draws.shape[1] - 1)].data_ptr()
             b.draw_plane_stride = self.draws.shape[1] * self.draws.shape[2]
             b.mt_state = self.mt_state[r0].data_ptr()
@@ -427,11 +432,11 @@ class BatchEngine:
         last = self.last_iteration(k)
         s = int(self.stopped[k])
         if s:   # absorbed at s: S_s, R_s untouched since; Q finalized by launch s
-            cur, qb = (s - 1) & 1, s & 1
+            cur = (s - 1) & 1
         else:   # S_{last+1}, R_{last+1}; Q finalized by the flush launch last+1
-            cur, qb = last & 1, (last + 1) & 1
+            cur = last & 1
         L = self.L
-        Qk = self.Qb[qb, k].cpu().numpy()
+        Qk = self.Qb[k].cpu().numpy()
         if self.double_q:   # q_table = mean of the two tables (algorithms.py:262-266)
             Q = ((Qk[:, :4] + Qk[:, 4:]) / 2).reshape(L, L, 2, 2)
         else:
@@ -444,9 +449,7 @@ class BatchEngine:
         """Double-Q: (q_table_1, q_table_2) of replica k after the run."""
         if not self.double_q:
             raise ValueError("final_tables: not a double_qlearning engine")
-        s = int(self.stopped[k])
-        qb = s & 1 if s else self.last_iteration(k) + 1 & 1
-        Qk = self.Qb[qb, k].cpu().numpy()
+        Qk = self.Qb[k].cpu().numpy()
         return Qk[:, :4].reshape(self.L, self.L, 2, 2).copy(), Qk[:, 4:].reshape(self.L, self.L, 2, 2).copy()
 
     def _rep_host(self, buf):

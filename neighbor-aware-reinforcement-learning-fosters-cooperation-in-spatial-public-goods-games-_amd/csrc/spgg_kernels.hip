@@ -36,6 +36,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "spgg_abi.h"
 #include "spgg_device.h"
@@ -78,8 +79,10 @@ struct TileArgs {
   double* stats;
   int* stop_iter;
   const spgg_rep_params* params;
+  const int2* ring;       // [tiles_per_rep][ring_max]: {agent index, border-record offset}
   int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
   int PB;                 // border-record slots per tile (pub_slots)
+  int ring_max;
 };
 
 // What a step launch needs to pick and size the kernel instance.
@@ -121,6 +124,26 @@ __host__ __device__ inline int border_slot(int r, int c, int th, int tw, int HA)
   return 2 * HA * tw + (r - HA) * 2 * HA + cc;
 }
 
+// Ring cell k of a th x tw tile in region coordinates (ay, ax) of the
+// (th + 2HA) x (tw + 2HA) window: the HA rows above, the HA rows below, then
+// HA cells left and right of each tile row.  k < (tw+2HA)(th+2HA) - th*tw.
+__host__ __device__ inline void ring_cell(int k, int th, int tw, int HA, int* ay, int* ax) {
+  const int aw = tw + 2 * HA, band = HA * aw;
+  if (k < band) {
+    *ay = k / aw;
+    *ax = k - *ay * aw;
+  } else if (k < 2 * band) {
+    const int k2 = k - band;
+    *ay = HA + th + k2 / aw;
+    *ax = k2 - (k2 / aw) * aw;
+  } else {
+    const int k3 = k - 2 * band;
+    *ay = HA + k3 / (2 * HA);
+    const int cc = k3 - (k3 / (2 * HA)) * (2 * HA);
+    *ax = cc < HA ? cc : tw + cc;
+  }
+}
+
 }  // namespace spgg_impl
 
 using spgg_impl::TileArgs;
@@ -132,7 +155,7 @@ constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_A, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_A, off_M, bytes;
 };
 
 // 16-byte aligned carve: f64 first, then the R planes (rsz = 8 or 1), then bytes.
@@ -148,6 +171,7 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_Rn = off;   off += ((na * rsz + 15) / 16) * 16;
   l.off_S = off;    off += ((l.sw * l.sh + 15) / 16) * 16;
   l.off_A = off;    off += ((na + 15) / 16) * 16;
+  l.off_M = off;    off += ((l.sh * 3 * 4 + 15) / 16) * 16;  // cooperator bitmask rows (3 dwords)
   l.bytes = off;
   return l;
 }
@@ -174,8 +198,22 @@ using RStore = typename std::conditional<RQ, int8_t, double>::type;
 template <bool RQ>
 using RVal = typename std::conditional<RQ, int, double>::type;
 
-template <bool RQ>
-__device__ __forceinline__ RVal<RQ> rep_next(RVal<RQ> r, int act, const spgg_rep_params& p) {
+// The per-agent fields of spgg_rep_params, copied to registers once per
+// workgroup (read through a reference into global memory the compiler must
+// assume the agents' stores may alias them and reloads them per agent).
+struct HotParams {
+  double norm_min, norm_den, norm_rcp, alpha, gamma, diag_alpha, diag_gamma;
+  double rep_gain_c, neg_delta_r_d, r_min, r_max;
+  int rk_gain, rk_loss, rk_min, rk_max;
+};
+
+__device__ __forceinline__ HotParams hot_params(const spgg_rep_params& p) {
+  return HotParams{p.norm_min, p.norm_den, p.norm_rcp, p.alpha, p.gamma, p.diag_alpha, p.diag_gamma,
+                   p.rep_gain_c, p.neg_delta_r_d, p.r_min, p.r_max, p.rk_gain, p.rk_loss, p.rk_min, p.rk_max};
+}
+
+template <bool RQ, typename PT>
+__device__ __forceinline__ RVal<RQ> rep_next(RVal<RQ> r, int act, const PT& p) {
   if constexpr (RQ) {  // spgg.py:321-323 in units of rep_unit
     const int k = r + (act == 0 ? p.rk_gain : -p.rk_loss);
     return min(max(k, p.rk_min), p.rk_max);
@@ -251,6 +289,11 @@ __device__ __forceinline__ int wrap1(int x, int L, bool tiny) {
 // is issued before the first LDS store: one memory round trip
 // (J >= h*w/kBlock; host-checked).  Measured 5% faster than one-row-per-wave
 // staging (lane-constant columns but 28% idle lanes at 46-wide rows).
+// Register type of a staged element: sub-dword values are held one per VGPR
+// (packing bytes with v_perm would make every load wait for the previous one).
+template <typename T>
+using StageReg = typename std::conditional<(sizeof(T) < 4), int, T>::type;
+
 template <int J, typename T>
 __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, int h, int w, int y0, int x0,
                                              int L, bool tiny) {
@@ -258,12 +301,14 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
   const int tid = threadIdx.x;
   const int dr = kBlock / w, dc = kBlock - (kBlock / w) * w;
   int r = tid / w, c = tid - (tid / w) * w;
-  T buf[J];
+  StageReg<T> buf[J];
   int di[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     di[j] = r * pitch + c;
-    if (tid + j * kBlock < total) buf[j] = src[wrap1(y0 + r, L, tiny) * L + wrap1(x0 + c, L, tiny)];
+    // unconditional load (tail rows clamped into the window): conditional loads
+    // make the compiler wait on each one before the next is issued
+    buf[j] = src[wrap1(y0 + min(r, h - 1), L, tiny) * L + wrap1(x0 + c, L, tiny)];
     r += dr;
     c += dc;
     if (c >= w) {
@@ -273,7 +318,7 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
   }
 #pragma unroll
   for (int j = 0; j < J; ++j)
-    if (tid + j * kBlock < total) dst[di[j]] = buf[j];
+    if (tid + j * kBlock < total) dst[di[j]] = (T)buf[j];
 }
 
 // Row-per-wave variant for a compile-time window width W <= 64 (TWC kernels,
@@ -281,36 +326,93 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
 // wave-uniform (scalar ALU), the column wrap is computed once per lane, so a
 // row costs ~3 vector instructions instead of ~30 for the flattened walk.
 template <int J, int W, int PITCH, typename T>
-__device__ __forceinline__ void stage_rows(T* dst, const T* src, int h, int y0, int x0, int L) {
+__device__ __forceinline__ void stage_rows(T* dst, const T* src, int h, int y0, int x0, int L,
+                                           uint32_t* coop_rows = nullptr) {
   static_assert(W <= 64, "one row per wave instruction");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int gx = x0 + lane;
+  const bool in_row = lane < W;
+  int gx = x0 + (in_row ? lane : W - 1);
   gx += gx < 0 ? L : 0;
   gx -= gx >= L ? L : 0;
-  const bool in_row = lane < W;
-  T buf[J];
+  StageReg<T> buf[J];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int row = wave + j * kWaves;
+  for (int j = 0; j < J; ++j) {  // unconditional loads (rows clamped): one round trip
+    const int row = min(wave + j * kWaves, h - 1);
     int gy = y0 + row;
     gy += gy < 0 ? L : 0;
     gy -= gy >= L ? L : 0;
-    if (in_row && row < h) buf[j] = src[gy * L + gx];
+    buf[j] = src[gy * L + gx];
   }
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int row = wave + j * kWaves;
-    if (in_row && row < h) dst[row * PITCH + lane] = buf[j];
+    if (in_row && row < h) dst[row * PITCH + lane] = (T)buf[j];
+    if constexpr (sizeof(T) == 1) {
+      if (coop_rows && row < h) {  // bit x = cooperator at window column x (S bit0 == 0)
+        const uint64_t m = __ballot(in_row && !(buf[j] & 1));
+        if (lane == 0) {
+          coop_rows[row * 3] = (uint32_t)m;
+          coop_rows[row * 3 + 1] = (uint32_t)(m >> 32);
+          coop_rows[row * 3 + 2] = 0u;
+        }
+      }
+    }
   }
+}
+
+// The same cooperator bitmask rows from an h x w byte window already in LDS
+// (flattened-staging path; w <= 64).
+__device__ __forceinline__ void coop_rows_from_lds(uint32_t* coop_rows, const uint8_t* s, int pitch, int h, int w) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int row = wave; row < h; row += kWaves) {
+    const bool in_row = lane < w;
+    const uint64_t m = __ballot(in_row && !(s[row * pitch + (in_row ? lane : 0)] & 1));
+    if (lane == 0) {
+      coop_rows[row * 3] = (uint32_t)m;
+      coop_rows[row * 3 + 1] = (uint32_t)(m >> 32);
+      coop_rows[row * 3 + 2] = 0u;
+    }
+  }
+}
+
+// Payoff of the agent at window row ry, column cx from the cooperator
+// bitmask rows (spgg.py:230-259, 373-377): the 5-cell windows of rows
+// ry-2..ry+2 packed into one 25-bit word X, each group count N_k one
+// popcount of X under a constant mask; then the reference's table sum.
+__device__ __forceinline__ double payoff_rows(const uint32_t* M, int ry, int cx, const double* tab,
+                                              double norm_min, double norm_den, double norm_rcp) {
+  const int s = cx - 2, sw = s >> 5, sb = s & 31;
+  const uint32_t* m = M + (ry - 2) * 3 + sw;
+  uint32_t X = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {  // row ry-2+k -> bits 5k..5k+4 (column cx-2+i -> bit i)
+    const uint32_t win = __builtin_amdgcn_alignbit(m[k * 3 + 1], m[k * 3], sb) & 31u;
+    X |= win << (5 * k);
+  }
+  constexpr uint32_t C = 0x4u;  // centre column bit of a 5-bit row window
+  constexpr uint32_t MN0 = (0xEu << 10) | (C << 5) | (C << 15);      // group (0,0)
+  constexpr uint32_t MN1 = (0xEu << 5) | C | (C << 10);              // group (1,0): centred at row -1
+  constexpr uint32_t MN2 = (0xEu << 15) | (C << 10) | (C << 20);     // group (-1,0): row +1
+  constexpr uint32_t MN3 = (0x7u << 10) | (0x2u << 5) | (0x2u << 15); // group (1,1): column -1
+  constexpr uint32_t MN4 = (0x1Cu << 10) | (0x8u << 5) | (0x8u << 15); // group (-1,1): column +1
+  const int c00 = (X >> 12) & 1;
+  const double* tb = tab + (c00 ? 0 : 6);
+  double tot = tb[__builtin_popcount(X & MN0)];
+  tot = tot + tb[__builtin_popcount(X & MN1)];
+  tot = tot + tb[__builtin_popcount(X & MN2)];
+  tot = tot + tb[__builtin_popcount(X & MN3)];
+  tot = tot + tb[__builtin_popcount(X & MN4)];
+  return div_uniform(tot - norm_min, norm_den, norm_rcp);  // (tot - (r-5)) / (4r - (r-5))
 }
 
 // Stage an h x w window: row-per-wave when the width is a compile-time
 // constant (TWC), else the flattened walk.
 template <int TWC, int HALO, int JF, int JR, typename T>
 __device__ __forceinline__ void stage(T* dst, int pitch, const T* src, int h, int w, int y0, int x0, int L,
-                                      bool tiny) {
-  if constexpr (TWC > 0) stage_rows<JR, TWC + 2 * HALO, TWC + 2 * HALO>(dst, src, h, y0, x0, L);
+                                      bool tiny, uint32_t* coop_rows = nullptr) {
+  if constexpr (TWC > 0) stage_rows<JR, TWC + 2 * HALO, TWC + 2 * HALO>(dst, src, h, y0, x0, L, coop_rows);
   else stage_region<JF>(dst, pitch, src, h, w, y0, x0, L, tiny);
 }
 
@@ -422,9 +524,9 @@ __device__ __forceinline__ void select_row(const double (&q)[4], const double (&
 // SARSA (whose diagnostic target is a fresh eps-greedy draw): |diag_alpha*td'|
 // with e = (s_old, a) and sn the new state.  Used right after the TD update
 // and again, on the same stored table, when the next launch recomputes it.
-template <int ALG>
+template <int ALG, typename PT>
 __device__ __forceinline__ float diag_td(const double (&q)[4], const double (&qb)[ALG == ALG_DQ ? 4 : 1], int e,
-                                         int sn, double rew, const spgg_rep_params& pg, double eps) {
+                                         int sn, double rew, const PT& pg, double eps) {
   double td2;
   if constexpr (ALG == ALG_DQ) {  // on the mean table (spgg.py:463-467)
     const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
@@ -441,8 +543,8 @@ __device__ __forceinline__ float diag_td(const double (&q)[4], const double (&qb
 
 // TD update of the operator for one agent (algorithms.py:112-341) and the
 // diagnostic TD on the updated table (spgg.py:446-473).  Returns |diag_alpha*td'|.
-template <int ALG, int RNG>
-__device__ __forceinline__ float td_update(const TileArgs& a, const spgg_rep_params& pg, size_t rb, int g, int t,
+template <int ALG, int RNG, typename PT>
+__device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size_t rb, int g, int t,
                                            uint32_t key, double eps, double rew, int so, int act, int sn,
                                            double (&q)[4], double (&qb)[ALG == ALG_DQ ? 4 : 1]) {
   const double alpha = pg.alpha, gamma = pg.gamma, dgamma = pg.diag_gamma;
@@ -547,8 +649,23 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   RT* Rout = reinterpret_cast<RT*>(a.R_out);
   uint8_t* sS = smem + ly.off_S;
   uint8_t* sA = smem + ly.off_A;
+  uint32_t* sM = reinterpret_cast<uint32_t*>(smem + ly.off_M);
 
+  // by value: uniform, lives in scalar registers (a reference into global memory may alias
+  // the stores below, and the compiler then reloads fields per agent with vector loads)
   const spgg_rep_params& pg = a.params[rep];
+#ifndef SPGG_HOT_LDS  // placement knob (A/B: 1 LDS 77.9, 0 registers 79.4, 2 global 80.6 us cfg3)
+#define SPGG_HOT_LDS 1
+#endif
+#if SPGG_HOT_LDS == 1  // per-agent fields in LDS (written before the staging barrier)
+  __shared__ HotParams hps;
+  if (threadIdx.x == 0) hps = hot_params(pg);
+  const HotParams& hp = hps;
+#elif SPGG_HOT_LDS == 2  // read through the global reference
+  const spgg_rep_params& hp = pg;
+#else
+  const HotParams hp = hot_params(pg);
+#endif
   const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
   double* srow = a.stats + (size_t)rep * a.slots * SPGG_NSTAT;
   bool stop_now = false;
@@ -589,13 +706,14 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       atd_own[u] = 0.f;
       q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
       if constexpr (QB) qb[u][0] = qb[u][1] = qb[u][2] = qb[u][3] = 0.0;
-      if (k < n_own) {
-        gidx[u] = (y0 + r) * L + (x0 + c);
-        load_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
-        if (pending) {
-          md_own[u] = a.md[rb + gidx[u]];
-          atd_own[u] = a.atd[rb + gidx[u]];
-        }
+      // loads unconditional (threads without a u-th agent read the tile's
+      // first one and drop it): conditional loads serialise on each other
+      const int g = k < n_own ? (y0 + r) * L + (x0 + c) : y0 * L + x0;
+      if (k < n_own) gidx[u] = g;
+      load_q<QB>(a.Q, rb + g, q[u], qb[u]);
+      if (pending) {
+        md_own[u] = a.md[rb + g];
+        atd_own[u] = a.atd[rb + g];
       }
       r += dr;
       c += dc;
@@ -605,13 +723,23 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       }
     }
   }
-  if (tid < 12) tab[tid] = tid < 6 ? pg.pay_c[tid] : pg.pay_d[tid - 6];
+  if (tid == 0) {  // scalar loads of the replica's payoff table (no vector-memory wait)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      tab[k] = pg.pay_c[k];
+      tab[6 + k] = pg.pay_d[k];
+    }
+  }
   // row-per-wave windows (TWC): rows <= TH + 2*halo with TH <= 25 (host-checked)
   constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
   constexpr int JSF = spgg_impl::js_of(M2), JRF = spgg_impl::jr_of();
-  stage<TWC, HS, JSF, JSR>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny);
+  stage<TWC, HS, JSF, JSR>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny, sM);
   if (!AS) stage<TWC, HA, JRF, JRR>(sR, ly.aw, Rin + rb, ah, aw, y0 - HA, x0 - HA, L, tiny);
   __syncthreads();
+  if constexpr (TWC == 0) {  // flattened staging: cooperator rows from the staged bytes
+    coop_rows_from_lds(sM, sS, ly.sw, th + 2 * HS, tw + 2 * HS);
+    __syncthreads();
+  }
   if (SPGG_ABLATE & 128) {  // memory floor: write back what was read
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
@@ -645,14 +773,18 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         const double nu = pending_nu(b, md_own[u], kappa, lam_den, lam_rcp);
         q_set(q[u], e, q_get(q[u], e) + nu);
         if constexpr (QB) q_set(qb[u], e, q_get(qb[u], e) + nu);  // both tables (spgg.py:496-502)
-        const double anu = fabs(nu);
-        v[0] += (anu * rcp_diag(((double)atd + anu) + 1e-8)) * 100.0;  // spgg.py:512
+        // NI percent (spgg.py:512; x100 applied to the workgroup total): exactly 0
+        // when kappa == 0 (nu = 0), a replica-uniform skip
+        if (kappa != 0.0) {
+          const double anu = fabs(nu);
+          v[0] += anu * rcp_diag(((double)atd + anu) + 1e-8);
+        }
         const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                  // prev_S of t-1 == C
 #pragma unroll
         for (int e2 = 0; e2 < 4; ++e2) {                                 // spgg.py:562-583
           const double qv = QB ? mean2(q[u][e2], qb[u][QB ? e2 : 0]) : q[u][e2];
           v[1 + e2] += qv;
-          v[5 + e2] += qv * cm;
+          v[5 + e2] = __builtin_fma(qv, cm, v[5 + e2]);                 // qv*cm exact: one rounding
         }
       }
     }
@@ -683,11 +815,11 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     const int cs = (r + HS) * ly.sw + (c + HS);
     const int ca = (r + HA) * ly.aw + (c + HA);
     const int s_t = sS[cs] & 1;
-    const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
+    const double P = payoff_rows(sM, r + HS, c + HS, tab, hp.norm_min, hp.norm_den, hp.norm_rcp);
     const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[ca];
     const double cmask = s_t ? 0.0 : 1.0;
     va[0] += P;                                           // spgg.py:388-390
-    va[1] += P * cmask;
+    va[1] = __builtin_fma(P, cmask, va[1]);
     va[2] += (double)r_t;                                 // spgg.py:394 (units if RQ)
     if (!acting) continue;
     int so;                                               // spgg.py:409
@@ -698,7 +830,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     double qs0, qs1;
     select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
     const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0
-    const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
+    const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
     const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
     const double wpp = w_p * P, wrr = w_rep * rr;
     const double rew = wpp + wrr;
@@ -714,8 +846,9 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     va[4] += wrr;
     va[5] += rew;                                         // spgg.py:529-545
     const double am = act ? 0.0 : 1.0;
-    va[6] += rew * am;
-    va[7] += ((fabs(wrr) * rcp_diag(fabs(rew) + 1e-9)) * 100.0) * am;
+    va[6] = __builtin_fma(rew, am, va[6]);
+    // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
+    if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
   }
 
   // ---- phase 1c: recompute the ring of neighbours (distance <= M) --------
@@ -723,32 +856,16 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   // border record of iteration t-1; the owner applies the same NI term to
   // the same entry, so both agree bit for bit.
   if (acting && !(SPGG_ABLATE & 4)) {
-    const int band = HA * aw;
     const int ring = aw * ah - n_own;
     const double* pin = a.pub_in + (size_t)rep * a.tiles_per_rep * PF * a.PB;
+    const int2* rtab = a.ring + (size_t)tile * a.ring_max;
     for (int k = tid; k < ring; k += kBlock) {
       int ay, ax;
-      if (k < band) {
-        ay = k / aw;
-        ax = k - ay * aw;
-      } else if (k < 2 * band) {
-        const int k2 = k - band;
-        ay = HA + th + k2 / aw;
-        ax = k2 - (k2 / aw) * aw;
-      } else {
-        const int k3 = k - 2 * band;
-        ay = HA + k3 / (2 * HA);
-        const int cc = k3 - (k3 / (2 * HA)) * (2 * HA);
-        ax = cc < HA ? cc : tw + cc;
-      }
-      const int gy = wrap1(y0 - HA + ay, L, tiny), gx = wrap1(x0 - HA + ax, L, tiny);
-      const int g = gy * L + gx;
-      // owner tile and border slot
-      const int oty = gy / a.TH, otx = gx / a.TW;
-      const int orr = gy - oty * a.TH, occ = gx - otx * a.TW;
-      const int oth = min(a.TH, L - oty * a.TH), otw = min(a.TW, L - otx * a.TW);
-      const double* rec = pin + (size_t)(oty * a.tiles_x + otx) * PF * a.PB +
-                          spgg_impl::border_slot(orr, occ, oth, otw, HA);
+      spgg_impl::ring_cell(k, th, tw, HA, &ay, &ax);
+      // agent index and owner's border record: geometry, precomputed per tile
+      const int2 re = rtab[k];
+      const int g = re.x;
+      const double* rec = pin + re.y;
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
       const uint8_t b = sS[cs];
       double v0 = rec[0], v1 = rec[a.PB], w0 = 0.0, w1 = 0.0;
@@ -766,12 +883,13 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
           }
         }
       }
-      const double P = payoff13(cells_at(sS, cs, ly.sw), tab, pg.norm_min, pg.norm_den, pg.norm_rcp);
+      const double P = payoff_rows(sM, ay + (HS - HA), ax + (HS - HA), tab, hp.norm_min, hp.norm_den,
+                                   hp.norm_rcp);
       const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sR[ay * ly.aw + ax]);
       int ex, rbt;
       draw_pair<RNG>(a, rb, g, t, pkey, eps_t, 0, &ex, &rbt);
       const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
-      const RVal<RQ> rn = rep_next<RQ>(r_t, act, pg);
+      const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
       const double rr = act == 0 ? 0.5 : 0.0;
       const double wpp = w_p * P, wrr = w_rep * rr;
       const int ca = ay * ly.aw + ax;
@@ -796,7 +914,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      const float atd = td_update<ALG, RNG>(a, pg, rb, gidx[u], t, pkey, eps_t, rew, so, act, sn, q[u], qb[u]);
+      const float atd = td_update<ALG, RNG>(a, hp, rb, gidx[u], t, pkey, eps_t, rew, so, act, sn, q[u], qb[u]);
       a.atd[rb + gidx[u]] = atd;
       store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
@@ -889,6 +1007,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
       if (counter) val = (double)(((unsigned long long)tot[0] >> (16 * ((j - 8) & 1))) & 0xffffu);
       if (RQ && k == SPGG_ST_SUMR) val *= pg.rep_unit;
+      if (k == SPGG_ST_SUM_PCT || k == SPGG_ST_SUM_RATIO_C) val *= 100.0;  // percent sums
       if (val != 0.0 && (!(SPGG_ABLATE & 2) || k == SPGG_ST_NCOOP))
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);
     }
@@ -1175,6 +1294,8 @@ struct spgg_ctx {
   bool bound = false;
   bool params_set = false;
   spgg_rep_params* d_params = nullptr;
+  int2* d_ring = nullptr;   // ring table (geometry of the tiling)
+  int ring_max = 0;
   int n = 0;
   int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4, PB = 0;
   size_t lds_bytes = 0;
@@ -1220,6 +1341,42 @@ void choose_tile(int L, int max_agents, int* TW, int* TH) {
 // Iteration t reads S_t, R_t, records [(t-1)&1] and writes [t&1]; Q, md,
 // atd in place.  t = 0 addresses the iteration-1 prologue (S_1 and R_1 in,
 // records [0] out).
+// For every tile, the ring cells in the kernel's enumeration order: the
+// agent index and the offset of its owner's border record (owner tile *
+// PF * PB + slot) within a replica's record buffer.
+int build_ring_table(spgg_ctx* c) {
+  const int L = c->cfg.L, HA = c->cfg.second_order ? 2 : 1;
+  const int PF = spgg_impl::pf_of(c->cfg.algorithm);
+  auto wrapL = [L](int x) { return ((x % L) + L) % L; };
+  int rmax = 1;
+  for (int tile = 0; tile < c->tiles_per_rep; ++tile) {
+    const int ty = tile / c->tiles_x, tx = tile % c->tiles_x;
+    const int th = std::min(c->TH, L - ty * c->TH), tw = std::min(c->TW, L - tx * c->TW);
+    rmax = std::max(rmax, (tw + 2 * HA) * (th + 2 * HA) - th * tw);
+  }
+  std::vector<int2> tab((size_t)c->tiles_per_rep * rmax, make_int2(0, 0));
+  for (int tile = 0; tile < c->tiles_per_rep; ++tile) {
+    const int ty = tile / c->tiles_x, tx = tile % c->tiles_x;
+    const int y0 = ty * c->TH, x0 = tx * c->TW;
+    const int th = std::min(c->TH, L - y0), tw = std::min(c->TW, L - x0);
+    const int ring = (tw + 2 * HA) * (th + 2 * HA) - th * tw;
+    for (int k = 0; k < ring; ++k) {
+      int ay, ax;
+      spgg_impl::ring_cell(k, th, tw, HA, &ay, &ax);
+      const int gy = wrapL(y0 - HA + ay), gx = wrapL(x0 - HA + ax);
+      const int oty = gy / c->TH, otx = gx / c->TW;
+      const int oth = std::min(c->TH, L - oty * c->TH), otw = std::min(c->TW, L - otx * c->TW);
+      const int slot = spgg_impl::border_slot(gy - oty * c->TH, gx - otx * c->TW, oth, otw, HA);
+      tab[(size_t)tile * rmax + k] = make_int2(gy * L + gx, (oty * c->tiles_x + otx) * PF * c->PB + slot);
+    }
+  }
+  c->ring_max = rmax;
+  int rc = hip_check(c, hipMalloc(&c->d_ring, tab.size() * sizeof(int2)), "hipMalloc(ring)");
+  if (rc) return rc;
+  return hip_check(c, hipMemcpy(c->d_ring, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice),
+                   "hipMemcpy(ring)");
+}
+
 TileArgs make_args(const spgg_ctx* c, int t) {
   TileArgs a{};
   if (t == 0) {
@@ -1250,6 +1407,8 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   a.n_rep = c->cfg.n_rep;
   a.slots = c->cfg.iterations + 2;
   a.PB = c->PB;
+  a.ring = c->d_ring;
+  a.ring_max = c->ring_max;
   return a;
 }
 
@@ -1329,8 +1488,9 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     return SPGG_E_ARG;
   }
   int rc = hip_check(c, hipSetDevice(cfg->device), "hipSetDevice");
+  if (!rc) rc = build_ring_table(c);
   if (rc) {
-    delete c;
+    spgg_destroy(c);
     return rc;
   }
   *out = c;
@@ -1429,9 +1589,10 @@ int spgg_tile_shape(const spgg_ctx* c, int32_t* tw, int32_t* th) {
 
 int spgg_destroy(spgg_ctx* c) {
   if (!c) return SPGG_OK;
-  if (c->d_params) {
+  if (c->d_params || c->d_ring) {
     (void)hipSetDevice(c->cfg.device);
-    (void)hipFree(c->d_params);
+    if (c->d_params) (void)hipFree(c->d_params);
+    if (c->d_ring) (void)hipFree(c->d_ring);
   }
   delete c;
   return SPGG_OK;

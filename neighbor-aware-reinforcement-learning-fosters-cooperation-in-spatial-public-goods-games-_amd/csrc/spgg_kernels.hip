@@ -102,6 +102,9 @@ constexpr int apt_of(int alg) { return (alg == SPGG_ALG_DOUBLE_Q ? 512 : 1024) /
 // tile of <= 1024 agents; host-checked).
 constexpr int js_of(bool m2) { return kBlock == 256 ? (m2 ? 8 : 7) : 4; }
 constexpr int jr_of() { return kBlock == 256 ? 6 : 3; }
+// Ring cells per thread: ring = (tw+2M)(th+2M) - tw*th <= 4M*(56+64)/2 + 4M^2 for
+// tiles of <= 1024 agents (host-checked against ring_max).
+constexpr int ring_per_thread(bool m2) { return kBlock == 256 && m2 ? 2 : 1; }
 // Doubles per agent in Q and fields per border record (Double-Q: both tables).
 constexpr int qw_of(int alg) { return alg == SPGG_ALG_DOUBLE_Q ? 8 : 4; }
 constexpr int pf_of(int alg) { return alg == SPGG_ALG_DOUBLE_Q ? 5 : 3; }
@@ -407,6 +410,50 @@ __device__ __forceinline__ double payoff_rows(const uint32_t* M, int ry, int cx,
   return div_uniform(tot - norm_min, norm_den, norm_rcp);  // (tot - (r-5)) / (4r - (r-5))
 }
 
+// Split form of stage_rows: load() issues the window's loads into registers,
+// store() (later, after other loads were issued) writes them to LDS.
+template <int J, int W, typename T>
+struct RowWindow {
+  StageReg<T> buf[J];
+  __device__ __forceinline__ void load(const T* src, int h, int y0, int x0, int L) {
+    static_assert(W <= 64, "one row per wave instruction");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int gx = x0 + (lane < W ? lane : W - 1);
+    gx += gx < 0 ? L : 0;
+    gx -= gx >= L ? L : 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {  // unconditional loads (rows clamped)
+      const int row = min(wave + j * kWaves, h - 1);
+      int gy = y0 + row;
+      gy += gy < 0 ? L : 0;
+      gy -= gy >= L ? L : 0;
+      buf[j] = src[gy * L + gx];
+    }
+  }
+  template <int PITCH>
+  __device__ __forceinline__ void store(T* dst, int h, uint32_t* coop_rows) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool in_row = lane < W;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int row = wave + j * kWaves;
+      if (in_row && row < h) dst[row * PITCH + lane] = (T)buf[j];
+      if constexpr (sizeof(T) == 1) {
+        if (coop_rows && row < h) {  // bit x = cooperator at window column x (S bit0 == 0)
+          const uint64_t m = __ballot(in_row && !(buf[j] & 1));
+          if (lane == 0) {
+            coop_rows[row * 3] = (uint32_t)m;
+            coop_rows[row * 3 + 1] = (uint32_t)(m >> 32);
+            coop_rows[row * 3 + 2] = 0u;
+          }
+        }
+      }
+    }
+  }
+};
+
 // Stage an h x w window: row-per-wave when the width is a compile-time
 // constant (TWC), else the flattened walk.
 template <int TWC, int HALO, int JF, int JR, typename T>
@@ -625,11 +672,9 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   const int per_xcd = (total + 7) / 8;
   const int logical = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (logical >= total) return;
+  if (SPGG_ABLATE & 64) return;
   const int rep = logical / a.tiles_per_rep;
   const int tile = logical - rep * a.tiles_per_rep;
-  const int st = a.stop_iter[rep];
-  if (st != 0 && st < t) return;  // absorbed before t
-  if (SPGG_ABLATE & 64) return;
 
   const int L = a.L, n = a.n;
   const bool tiny = TWC ? false : L < 8;  // TWC => L % TWC == 0
@@ -650,43 +695,15 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   uint8_t* sS = smem + ly.off_S;
   uint8_t* sA = smem + ly.off_A;
   uint32_t* sM = reinterpret_cast<uint32_t*>(smem + ly.off_M);
-
-  // by value: uniform, lives in scalar registers (a reference into global memory may alias
-  // the stores below, and the compiler then reloads fields per agent with vector loads)
-  const spgg_rep_params& pg = a.params[rep];
-#ifndef SPGG_HOT_LDS  // placement knob (A/B: 1 LDS 77.9, 0 registers 79.4, 2 global 80.6 us cfg3)
-#define SPGG_HOT_LDS 1
-#endif
-#if SPGG_HOT_LDS == 1  // per-agent fields in LDS (written before the staging barrier)
-  __shared__ HotParams hps;
-  if (threadIdx.x == 0) hps = hot_params(pg);
-  const HotParams& hp = hps;
-#elif SPGG_HOT_LDS == 2  // read through the global reference
-  const spgg_rep_params& hp = pg;
-#else
-  const HotParams hp = hot_params(pg);
-#endif
-  const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
-  double* srow = a.stats + (size_t)rep * a.slots * SPGG_NSTAT;
-  bool stop_now = false;
-  if (!fin_only) {
-    const double nc = srow[(size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
-    stop_now = (nc == 0.0) || (nc == (double)n);  // spgg.py:405
-    if (stop_now && tile == 0 && threadIdx.x == 0) a.stop_iter[rep] = t;
-  }
-  const bool acting = !fin_only && !stop_now;
   const bool pending = t > 1;
-  const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
-  const double lam_rcp = 1.0 / lam_den;  // IEEE, once per workgroup
-  const double eps_t = a.eps[(size_t)rep * a.slots + t];
   const size_t rb = (size_t)rep * n;
   const int tid = threadIdx.x;
-  // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
-  const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
-                        (uint32_t)pg.stream_id * 0xC2B2AE35u;
   const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
 
-  // ---- phase 0: owned-agent registers + LDS staging ----------------------
+  // ---- phase 0: every vector load first, then the replica's state ---------
+  // None of these loads depends on the replica's state, so they are all in
+  // flight together (one memory round trip) while the scalar reads below
+  // (stop flag, counters, parameters) resolve.
   // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
   int gidx[APT], rc[APT];
   double q[APT][4];
@@ -723,6 +740,41 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       }
     }
   }
+  // ring cells of this thread (k = tid + j*kBlock): agent index + border-record offset
+  constexpr int RP = spgg_impl::ring_per_thread(M2);
+  const int ring = aw * ah - n_own;
+  int2 re[RP];
+  {
+    const int2* rtab = a.ring + (size_t)tile * a.ring_max;
+#pragma unroll
+    for (int j = 0; j < RP; ++j) re[j] = rtab[min(tid + j * kBlock, ring - 1)];
+  }
+  // halo windows into registers (TWC: row-per-wave; rows <= TH + 2*halo, TH <= 25 host-checked)
+  constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
+  constexpr int JSF = spgg_impl::js_of(M2), JRF = spgg_impl::jr_of();
+  RowWindow<JSR, TWC + 2 * HS, uint8_t> winS;
+  RowWindow<JRR, TWC + 2 * HA, RT> winR;
+  if constexpr (TWC > 0) {
+    winS.load(a.S_in + rb, th + 2 * HS, y0 - HS, x0 - HS, L);
+    if (!AS) winR.load(Rin + rb, ah, y0 - HA, x0 - HA, L);
+  }
+
+  // replica state (scalar loads)
+  const int st = a.stop_iter[rep];
+  const bool dead = st != 0 && st < t;  // absorbed before t: nothing to do
+  const spgg_rep_params& pg = a.params[rep];
+#ifndef SPGG_HOT_LDS  // placement knob (A/B: 1 LDS 77.9, 0 registers 79.4, 2 global 80.6 us cfg3)
+#define SPGG_HOT_LDS 1
+#endif
+#if SPGG_HOT_LDS == 1  // per-agent fields in LDS (written before the staging barrier)
+  __shared__ HotParams hps;
+  if (tid == 0) hps = hot_params(pg);
+  const HotParams& hp = hps;
+#elif SPGG_HOT_LDS == 2  // read through the global reference
+  const spgg_rep_params& hp = pg;
+#else
+  const HotParams hp = hot_params(pg);
+#endif
   if (tid == 0) {  // scalar loads of the replica's payoff table (no vector-memory wait)
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -730,11 +782,42 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       tab[6 + k] = pg.pay_d[k];
     }
   }
-  // row-per-wave windows (TWC): rows <= TH + 2*halo with TH <= 25 (host-checked)
-  constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
-  constexpr int JSF = spgg_impl::js_of(M2), JRF = spgg_impl::jr_of();
-  stage<TWC, HS, JSF, JSR>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny, sM);
-  if (!AS) stage<TWC, HA, JRF, JRR>(sR, ly.aw, Rin + rb, ah, aw, y0 - HA, x0 - HA, L, tiny);
+  const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
+  double* srow = a.stats + (size_t)rep * a.slots * SPGG_NSTAT;
+  bool stop_now = false;
+  if (!fin_only) {
+    const double nc = srow[(size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
+    stop_now = (nc == 0.0) || (nc == (double)n);  // spgg.py:405
+  }
+  const bool acting = !fin_only && !stop_now;
+  const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
+  const double lam_rcp = 1.0 / lam_den;  // IEEE, once per workgroup
+  const double eps_t = a.eps[(size_t)rep * a.slots + t];
+  // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
+  const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
+                        (uint32_t)pg.stream_id * 0xC2B2AE35u;
+
+  // windows -> LDS (waits for the loads above)
+  if constexpr (TWC > 0) {
+    winS.template store<TWC + 2 * HS>(sS, th + 2 * HS, sM);
+    if (!AS) winR.template store<TWC + 2 * HA>(sR, ah, nullptr);
+  } else {
+    stage_region<JSF>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny);
+    if (!AS) stage_region<JRF>(sR, ly.aw, Rin + rb, ah, aw, y0 - HA, x0 - HA, L, tiny);
+  }
+  if (dead) return;  // workgroup-uniform; no vector load is outstanding here
+  if (stop_now && tile == 0 && tid == 0) a.stop_iter[rep] = t;
+  // border records of this thread's ring cells: in flight during phases 1a / 1b
+  // (unconditional: every offset is valid, and a load under a branch makes the
+  // compiler wait for it at the join)
+  double rv[RP][PF];
+  {
+    const double* pin = a.pub_in + (size_t)rep * a.tiles_per_rep * PF * a.PB;
+#pragma unroll
+    for (int j = 0; j < RP; ++j)
+#pragma unroll
+      for (int f = 0; f < PF; ++f) rv[j][f] = pin[re[j].y + f * a.PB];
+  }
   __syncthreads();
   if constexpr (TWC == 0) {  // flattened staging: cooperator rows from the staged bytes
     coop_rows_from_lds(sM, sS, ly.sw, th + 2 * HS, tw + 2 * HS);
@@ -753,8 +836,6 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     }
     return;
   }
-
-  __syncthreads();
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
   // value slots: 0 pct, 1-4 sum Q, 5-8 sum Q over prev C  (-> slot t-1)
@@ -856,27 +937,24 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   // border record of iteration t-1; the owner applies the same NI term to
   // the same entry, so both agree bit for bit.
   if (acting && !(SPGG_ABLATE & 4)) {
-    const int ring = aw * ah - n_own;
-    const double* pin = a.pub_in + (size_t)rep * a.tiles_per_rep * PF * a.PB;
-    const int2* rtab = a.ring + (size_t)tile * a.ring_max;
-    for (int k = tid; k < ring; k += kBlock) {
+#pragma unroll
+    for (int j = 0; j < RP; ++j) {
+      const int k = tid + j * kBlock;
+      if (k >= ring) break;
       int ay, ax;
       spgg_impl::ring_cell(k, th, tw, HA, &ay, &ax);
-      // agent index and owner's border record: geometry, precomputed per tile
-      const int2 re = rtab[k];
-      const int g = re.x;
-      const double* rec = pin + re.y;
+      const int g = re[j].x;
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
       const uint8_t b = sS[cs];
-      double v0 = rec[0], v1 = rec[a.PB], w0 = 0.0, w1 = 0.0;
+      double v0 = rv[j][0], v1 = rv[j][1], w0 = 0.0, w1 = 0.0;
       if constexpr (QB) {
-        w0 = rec[2 * a.PB];
-        w1 = rec[3 * a.PB];
+        w0 = rv[j][QB ? 2 : 0];
+        w1 = rv[j][QB ? 3 : 0];
       }
       if (pending) {
         const int e = pending_entry(b);
         if ((e >> 1) == ((b >> 4) & 1)) {  // the NI entry lies in the published row
-          const double nu = pending_nu(b, rec[(PF - 1) * a.PB], kappa, lam_den, lam_rcp);
+          const double nu = pending_nu(b, rv[j][PF - 1], kappa, lam_den, lam_rcp);
           if (e & 1) v1 = v1 + nu; else v0 = v0 + nu;
           if constexpr (QB) {
             if (e & 1) w1 = w1 + nu; else w0 = w0 + nu;
@@ -1370,6 +1448,8 @@ int build_ring_table(spgg_ctx* c) {
       tab[(size_t)tile * rmax + k] = make_int2(gy * L + gx, (oty * c->tiles_x + otx) * PF * c->PB + slot);
     }
   }
+  if (rmax > spgg_impl::ring_per_thread(c->cfg.second_order != 0) * kBlock)
+    return fail(c, SPGG_E_ARG, "tile ring exceeds the kernel's ring cells per thread");
   c->ring_max = rmax;
   int rc = hip_check(c, hipMalloc(&c->d_ring, tab.size() * sizeof(int2)), "hipMalloc(ring)");
   if (rc) return rc;

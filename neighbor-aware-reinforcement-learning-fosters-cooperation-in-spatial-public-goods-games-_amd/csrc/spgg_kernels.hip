@@ -705,7 +705,12 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   // flight together (one memory round trip) while the scalar reads below
   // (stop flag, counters, parameters) resolve.
   // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
+  // Agent slots are branch-free: a slot past the tile's last agent SHADOWS the
+  // tile's first agent (same inputs, so every value it computes and stores is
+  // bit-identical to the owner's); only its history contributions are masked
+  // (vm = 0).  Per-slot branches cost more in exec-mask and copy instructions.
   int gidx[APT], rc[APT];
+  double vm[APT];
   double q[APT][4];
   double qb[APT][QB ? 4 : 1];
   double md_own[APT];
@@ -717,16 +722,17 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int k = tid + u * kBlock;
-      gidx[u] = -1;
-      rc[u] = (r << 16) | c;
+      const bool own = k < n_own;
+      rc[u] = own ? (r << 16) | c : 0;
+      vm[u] = own ? 1.0 : 0.0;
       md_own[u] = 0.0;
       atd_own[u] = 0.f;
       q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
       if constexpr (QB) qb[u][0] = qb[u][1] = qb[u][2] = qb[u][3] = 0.0;
       // loads unconditional (threads without a u-th agent read the tile's
       // first one and drop it): conditional loads serialise on each other
-      const int g = k < n_own ? (y0 + r) * L + (x0 + c) : y0 * L + x0;
-      if (k < n_own) gidx[u] = g;
+      const int g = own ? (y0 + r) * L + (x0 + c) : y0 * L + x0;
+      gidx[u] = g;
       load_q<QB>(a.Q, rb + g, q[u], qb[u]);
       if (pending) {
         md_own[u] = a.md[rb + g];
@@ -826,7 +832,6 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   if (SPGG_ABLATE & 128) {  // memory floor: write back what was read
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
-      if (gidx[u] < 0) continue;
       const int r = rc[u] >> 16, c = rc[u] & 0xffff;
       store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
       a.md[rb + gidx[u]] = md_own[u];
@@ -846,7 +851,6 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     if (pending) {
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
-        if (gidx[u] < 0) continue;
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
         const int e = pending_entry(b);
@@ -858,14 +862,14 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         // when kappa == 0 (nu = 0), a replica-uniform skip
         if (kappa != 0.0) {
           const double anu = fabs(nu);
-          v[0] += anu * rcp_diag(((double)atd + anu) + 1e-8);
+          v[0] = __builtin_fma(anu * rcp_diag(((double)atd + anu) + 1e-8), vm[u], v[0]);
         }
-        const double cm = ((b >> 3) & 1) ? 0.0 : 1.0;                  // prev_S of t-1 == C
+        const double cm = ((b >> 3) & 1) ? 0.0 : vm[u];                // prev_S of t-1 == C
 #pragma unroll
         for (int e2 = 0; e2 < 4; ++e2) {                                 // spgg.py:562-583
           const double qv = QB ? mean2(q[u][e2], qb[u][QB ? e2 : 0]) : q[u][e2];
-          v[1 + e2] += qv;
-          v[5 + e2] = __builtin_fma(qv, cm, v[5 + e2]);                 // qv*cm exact: one rounding
+          v[1 + e2] = __builtin_fma(qv, vm[u], v[1 + e2]);             // x*0/1 exact: one rounding
+          v[5 + e2] = __builtin_fma(qv, cm, v[5 + e2]);
         }
       }
     }
@@ -873,10 +877,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
-    for (int u = 0; u < APT; ++u) {
-      if (gidx[u] < 0) continue;
-      store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
-    }
+    for (int u = 0; u < APT; ++u) store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
   }
 
   // ---- phase 1b: iteration start + action select for owned agents --------
@@ -891,17 +892,18 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
 #pragma unroll
   for (int u = 0; u < APT; ++u) {
     own_bits[u] = 0;
-    if (fin_only || gidx[u] < 0) continue;
+    if (fin_only) continue;
     const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+    const uint32_t one = vm[u] != 0.0 ? 1u : 0u;
     const int cs = (r + HS) * ly.sw + (c + HS);
     const int ca = (r + HA) * ly.aw + (c + HA);
     const int s_t = sS[cs] & 1;
     const double P = payoff_rows(sM, r + HS, c + HS, tab, hp.norm_min, hp.norm_den, hp.norm_rcp);
     const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[ca];
-    const double cmask = s_t ? 0.0 : 1.0;
-    va[0] += P;                                           // spgg.py:388-390
+    const double cmask = s_t ? 0.0 : vm[u];
+    va[0] = __builtin_fma(P, vm[u], va[0]);               // spgg.py:388-390
     va[1] = __builtin_fma(P, cmask, va[1]);
-    va[2] += (double)r_t;                                 // spgg.py:394 (units if RQ)
+    va[2] = __builtin_fma((double)r_t, vm[u], va[2]);     // spgg.py:394 (units if RQ)
     if (!acting) continue;
     int so;                                               // spgg.py:409
     if constexpr (AS) so = s_t == 0 ? 1 : 0;
@@ -920,13 +922,13 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     sRew[ca] = rew;
     Rout[rb + gidx[u]] = (RT)rn;
     own_bits[u] = act | (so << 1) | (s_t << 3);
-    cw0 += (s_t == 0 && act == 1) ? 1u : 0u;             // spgg.py:419-420
-    cw0 += (s_t == 1 && act == 0) ? 0x10000u : 0u;
-    cw1 += act == 0 ? 1u : 0u;
-    va[3] += wpp;                                         // spgg.py:425-426
-    va[4] += wrr;
-    va[5] += rew;                                         // spgg.py:529-545
-    const double am = act ? 0.0 : 1.0;
+    cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
+    cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
+    cw1 += act == 0 ? one : 0u;
+    va[3] = __builtin_fma(wpp, vm[u], va[3]);             // spgg.py:425-426
+    va[4] = __builtin_fma(wrr, vm[u], va[4]);
+    va[5] = __builtin_fma(rew, vm[u], va[5]);             // spgg.py:529-545
+    const double am = act ? 0.0 : vm[u];
     va[6] = __builtin_fma(rew, am, va[6]);
     // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
     if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
@@ -984,9 +986,9 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     double* pout = a.pub_out + (size_t)(rep * a.tiles_per_rep + tile) * PF * a.PB;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
-      if (gidx[u] < 0) continue;
       const int r = rc[u] >> 16, c = rc[u] & 0xffff;
       const int ca = (r + HA) * ly.aw + (c + HA);
+      const uint32_t one = vm[u] != 0.0 ? 1u : 0u;
       const int act = own_bits[u] & 1, so = (own_bits[u] >> 1) & 1;
       const double rew = sRew[ca];
       int sn;                                               // spgg.py:423
@@ -1002,17 +1004,16 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
                           ca - 2 * w, ca + 2 * w, ca - 2, ca + 2,
                           ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
       double md = sRew[nb[0]] - rew;
-      int sel = nb[0], ks = 0;
+      int abest = sA[nb[0]], ks = 0;  // best neighbour's action (and offset index, M=2)
 #pragma unroll
       for (int kk = 1; kk < KN; ++kk) {
         const double d = sRew[nb[kk]] - rew;
-        if (d > md) {
-          md = d;
-          sel = nb[kk];
-          ks = kk;
-        }
+        const bool better = d > md;
+        md = better ? d : md;
+        abest = better ? (int)sA[nb[kk]] : abest;
+        if constexpr (M2) ks = better ? kk : ks;
       }
-      const int dp = sA[sel] == act ? 1 : 0;
+      const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = fmax(bmax, mdp);
       a.md[rb + gidx[u]] = mdp;
@@ -1029,11 +1030,11 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       }
       // group composition on S_{t+1}, spgg.py:585-592
       const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
-      if (nd < 3) cwa += 1ull << (16 * (nd + 1));          // GC0..2: fields 5-7
-      else cwb += 1ull << (16 * (nd - 3));                  // GC3..5: fields 8-10
+      if (nd < 3) cwa += (uint64_t)one << (16 * (nd + 1));  // GC0..2: fields 5-7
+      else cwb += (uint64_t)one << (16 * (nd - 3));         // GC3..5: fields 8-10
       if (md > 0.0) {                                       // spgg.py:520-523
-        cw1 += 0x10000u;
-        if (ks >= 4) cwa += 1u;
+        cw1 += one << 16;
+        if (M2 && ks >= 4) cwa += one;
       }
     }
   }
@@ -1416,9 +1417,6 @@ void choose_tile(int L, int max_agents, int* TW, int* TH) {
   *TH = best_h;
 }
 
-// Iteration t reads S_t, R_t, records [(t-1)&1] and writes [t&1]; Q, md,
-// atd in place.  t = 0 addresses the iteration-1 prologue (S_1 and R_1 in,
-// records [0] out).
 // For every tile, the ring cells in the kernel's enumeration order: the
 // agent index and the offset of its owner's border record (owner tile *
 // PF * PB + slot) within a replica's record buffer.
@@ -1457,6 +1455,9 @@ int build_ring_table(spgg_ctx* c) {
                    "hipMemcpy(ring)");
 }
 
+// Iteration t reads S_t, R_t, records [(t-1)&1] and writes [t&1]; Q, md,
+// atd in place.  t = 0 addresses the iteration-1 prologue (S_1 and R_1 in,
+// records [0] out).
 TileArgs make_args(const spgg_ctx* c, int t) {
   TileArgs a{};
   if (t == 0) {

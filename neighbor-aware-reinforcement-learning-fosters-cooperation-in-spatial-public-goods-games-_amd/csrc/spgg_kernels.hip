@@ -46,7 +46,8 @@ using namespace spgg;
 // Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
-//   128 = memory only (the owned loads, staging and stores, no compute)
+//   128 = memory only (the owned loads, staging and stores, no compute),
+//   256 / 512 = Philox / payoff computed twice (value-preserving: marginal-cost probes)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
@@ -384,8 +385,21 @@ __device__ __forceinline__ void coop_rows_from_lds(uint32_t* coop_rows, const ui
 // bitmask rows (spgg.py:230-259, 373-377): the 5-cell windows of rows
 // ry-2..ry+2 packed into one 25-bit word X, each group count N_k one
 // popcount of X under a constant mask; then the reference's table sum.
+__device__ __forceinline__ double payoff_rows_(const uint32_t* M, int ry, int cx, const double* tab,
+                                               double norm_min, double norm_den, double norm_rcp);
 __device__ __forceinline__ double payoff_rows(const uint32_t* M, int ry, int cx, const double* tab,
                                               double norm_min, double norm_den, double norm_rcp) {
+#if SPGG_ABLATE & 512
+  int ry2 = ry;
+  asm volatile("" : "+v"(ry2));
+  return (payoff_rows_(M, ry, cx, tab, norm_min, norm_den, norm_rcp) +
+          payoff_rows_(M, ry2, cx, tab, norm_min, norm_den, norm_rcp)) * 0.5;
+#else
+  return payoff_rows_(M, ry, cx, tab, norm_min, norm_den, norm_rcp);
+#endif
+}
+__device__ __forceinline__ double payoff_rows_(const uint32_t* M, int ry, int cx, const double* tab,
+                                               double norm_min, double norm_den, double norm_rcp) {
   const int s = cx - 2, sw = s >> 5, sb = s & 31;
   const uint32_t* m = M + (ry - 2) * 3 + sw;
   uint32_t X = 0;
@@ -510,6 +524,14 @@ __device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, i
     *ex = ((g * 2654435761u + t + k) >> 7) % 50 == 0; *rbt = (g ^ t ^ k) & 1;
 #else
     philox_draw(g, t + (k << 26), key, thr, ex, rbt);
+#if SPGG_ABLATE & 256
+    int g2 = g;
+    asm volatile("" : "+v"(g2));
+    int ex2, rbt2;
+    philox_draw(g2, t + (k << 26), key, thr, &ex2, &rbt2);
+    *ex = *ex & ex2;
+    *rbt = *rbt & rbt2;
+#endif
 #endif
   } else {
     *ex = a.draws[(size_t)(2 * k) * a.plane + rb + g];
@@ -710,7 +732,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   // bit-identical to the owner's); only its history contributions are masked
   // (vm = 0).  Per-slot branches cost more in exec-mask and copy instructions.
   int gidx[APT], rc[APT];
-  double vm[APT];
+  unsigned vbits = 0;  // bit u: slot u holds an owned agent
   double q[APT][4];
   double qb[APT][QB ? 4 : 1];
   double md_own[APT];
@@ -724,7 +746,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       const int k = tid + u * kBlock;
       const bool own = k < n_own;
       rc[u] = own ? (r << 16) | c : 0;
-      vm[u] = own ? 1.0 : 0.0;
+      vbits |= own ? 1u << u : 0u;
       md_own[u] = 0.0;
       atd_own[u] = 0.f;
       q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
@@ -843,14 +865,15 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   }
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
-  // value slots: 0 pct, 1-4 sum Q, 5-8 sum Q over prev C  (-> slot t-1)
+  // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C, 8 NI percent
   {
-    double v[16];
+    double v[8], pct = 0.0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = 0.0;
+    for (int k = 0; k < 8; ++k) v[k] = 0.0;
     if (pending) {
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
+        const double vmu = (vbits >> u) & 1 ? 1.0 : 0.0;
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
         const int e = pending_entry(b);
@@ -862,18 +885,20 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         // when kappa == 0 (nu = 0), a replica-uniform skip
         if (kappa != 0.0) {
           const double anu = fabs(nu);
-          v[0] = __builtin_fma(anu * rcp_diag(((double)atd + anu) + 1e-8), vm[u], v[0]);
+          pct = __builtin_fma(anu * rcp_diag(((double)atd + anu) + 1e-8), vmu, pct);
         }
-        const double cm = ((b >> 3) & 1) ? 0.0 : vm[u];                // prev_S of t-1 == C
+        const double cm = ((b >> 3) & 1) ? 0.0 : vmu;                  // prev_S of t-1 == C
 #pragma unroll
         for (int e2 = 0; e2 < 4; ++e2) {                                 // spgg.py:562-583
           const double qv = QB ? mean2(q[u][e2], qb[u][QB ? e2 : 0]) : q[u][e2];
-          v[1 + e2] = __builtin_fma(qv, vm[u], v[1 + e2]);             // x*0/1 exact: one rounding
-          v[5 + e2] = __builtin_fma(qv, cm, v[5 + e2]);
+          v[e2] = __builtin_fma(qv, vmu, v[e2]);                        // x*0/1 exact: one rounding
+          v[4 + e2] = __builtin_fma(qv, cm, v[4 + e2]);
         }
       }
     }
-    wave_partials<16>(v, red, 0);
+    wave_partials<8>(v, red, 0);
+    double pv[1] = {pct};
+    wave_partials<1>(pv, red, 8);
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
@@ -894,16 +919,17 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     own_bits[u] = 0;
     if (fin_only) continue;
     const int r = rc[u] >> 16, c = rc[u] & 0xffff;
-    const uint32_t one = vm[u] != 0.0 ? 1u : 0u;
+    const uint32_t one = (vbits >> u) & 1;
+    const double vmu = one ? 1.0 : 0.0;
     const int cs = (r + HS) * ly.sw + (c + HS);
     const int ca = (r + HA) * ly.aw + (c + HA);
     const int s_t = sS[cs] & 1;
     const double P = payoff_rows(sM, r + HS, c + HS, tab, hp.norm_min, hp.norm_den, hp.norm_rcp);
     const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[ca];
-    const double cmask = s_t ? 0.0 : vm[u];
-    va[0] = __builtin_fma(P, vm[u], va[0]);               // spgg.py:388-390
+    const double cmask = s_t ? 0.0 : vmu;
+    va[0] = __builtin_fma(P, vmu, va[0]);                 // spgg.py:388-390
     va[1] = __builtin_fma(P, cmask, va[1]);
-    va[2] = __builtin_fma((double)r_t, vm[u], va[2]);     // spgg.py:394 (units if RQ)
+    va[2] = __builtin_fma((double)r_t, vmu, va[2]);       // spgg.py:394 (units if RQ)
     if (!acting) continue;
     int so;                                               // spgg.py:409
     if constexpr (AS) so = s_t == 0 ? 1 : 0;
@@ -925,10 +951,10 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
     cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
     cw1 += act == 0 ? one : 0u;
-    va[3] = __builtin_fma(wpp, vm[u], va[3]);             // spgg.py:425-426
-    va[4] = __builtin_fma(wrr, vm[u], va[4]);
-    va[5] = __builtin_fma(rew, vm[u], va[5]);             // spgg.py:529-545
-    const double am = act ? 0.0 : vm[u];
+    va[3] = __builtin_fma(wpp, vmu, va[3]);               // spgg.py:425-426
+    va[4] = __builtin_fma(wrr, vmu, va[4]);
+    va[5] = __builtin_fma(rew, vmu, va[5]);               // spgg.py:529-545
+    const double am = act ? 0.0 : vmu;
     va[6] = __builtin_fma(rew, am, va[6]);
     // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
     if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
@@ -988,7 +1014,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = rc[u] & 0xffff;
       const int ca = (r + HA) * ly.aw + (c + HA);
-      const uint32_t one = vm[u] != 0.0 ? 1u : 0u;
+      const uint32_t one = (vbits >> u) & 1;
       const int act = own_bits[u] & 1, so = (own_bits[u] >> 1) & 1;
       const double rew = sRew[ca];
       int sn;                                               // spgg.py:423
@@ -1054,10 +1080,10 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     if (tid < 13) {
       if (pending) {
         slot = t - 1;
-        if (tid == 0) { k = SPGG_ST_SUM_PCT; src = 0; }
-        else if (tid < 5) { k = SPGG_ST_SUMQ + tid - 1; src = tid; }
-        else if (tid < 9) { k = SPGG_ST_SUMQ_C + tid - 5; src = tid; }
-        else { k = SPGG_ST_SUMQ_D + tid - 9; src = tid - 8; src_c = tid - 4; }
+        if (tid < 4) { k = SPGG_ST_SUMQ + tid; src = tid; }
+        else if (tid < 8) { k = SPGG_ST_SUMQ_C + tid - 4; src = tid; }
+        else if (tid == 8) { k = SPGG_ST_SUM_PCT; src = 8; }
+        else { k = SPGG_ST_SUMQ_D + tid - 9; src = tid - 9; src_c = tid - 5; }
       }
     } else if (tid >= 16 && tid < 16 + 22 && !fin_only) {
       const int j = tid - 16;  // 0-7 va, 8-18 counters, 19-20 derived

@@ -181,14 +181,22 @@ __device__ __forceinline__ uint2 philox2x32_10(uint2 c, uint32_t k) {
   return c;
 }
 
+// u < thr for u = k / 2^53 (k < 2^53, numpy's random_sample) and a threshold
+// in [0, 1] given as T = ceil(thr * 2^53): the scaling by 2^53 is exact, and
+// for an integer k, k < x <=> k < ceil(x).  One 64-bit integer compare.
+__host__ __device__ inline uint64_t u53_threshold(double thr) {
+  return (uint64_t)__builtin_ceil(thr * 9007199254740992.0);
+}
+
 // eps-greedy draw of agent `idx` at iteration t (Philox mode): counter
 // (agent, iteration), key = replica seed mixed with the replica index.
 // u takes 53 bits (w.x>>5, w.y>>6) exactly as numpy's random_sample; the
 // random action is the low bit of w.y, which u does not use.
-__device__ __forceinline__ void philox_draw(int idx, int t, uint32_t key, double eps, int* explore,
+__device__ __forceinline__ void philox_draw(int idx, int t, uint32_t key, uint64_t thr53, int* explore,
                                             int* rbit) {
   const uint2 w = philox2x32_10(make_uint2((uint32_t)idx, (uint32_t)t), key);
-  *explore = mt_double(w.x, w.y) < eps ? 1 : 0;  // algorithms.py:105
+  const uint64_t k = ((uint64_t)(w.x >> 5) << 26) | (w.y >> 6);
+  *explore = k < thr53 ? 1 : 0;                   // algorithms.py:105 (rand < eps)
   *rbit = (int)(w.y & 1u);                        // algorithms.py:108
 }
 

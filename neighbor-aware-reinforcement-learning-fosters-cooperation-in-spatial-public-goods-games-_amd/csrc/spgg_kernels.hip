@@ -263,7 +263,7 @@ __device__ __forceinline__ int rep_state_lds(const double* R, int c, int w) {
 // +-1 by whether the best neighbour's action matched (S_t bit 2).
 __device__ __forceinline__ double pending_nu(uint8_t b, double md, double kappa, double lam_den, double lam_rcp) {
   const double lam = div_uniform(kappa * md, lam_den, lam_rcp);  // (kappa*max(0,md))/(gmax+eps)
-  return lam * (((b >> 2) & 1) ? 1.0 : -1.0);
+  return ((b >> 2) & 1) ? lam : -lam;  // lam * (+-1.0): exact sign flip
 }
 
 // (s_old, a) entry index of iteration t-1 recorded in S_t bits 0-1.
@@ -517,7 +517,7 @@ __device__ __forceinline__ double expected_q(double v0, double v1, double eps) {
 // randint bit.  Philox: counter (agent, t + k*2^26) under the replica key;
 // device MT19937 / inject: planes 2k, 2k+1 of the draw record.
 template <int RNG>
-__device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, int t, uint32_t key, double thr,
+__device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, int t, uint32_t key, uint64_t thr,
                                           int k, int* ex, int* rbt) {
   if constexpr (RNG == SPGG_RNG_PHILOX) {
 #if SPGG_ABLATE & 1
@@ -544,7 +544,7 @@ template <int RNG>
 __device__ __forceinline__ int draw_table1(const TileArgs& a, size_t rb, int g, int t, uint32_t key) {
   if constexpr (RNG == SPGG_RNG_PHILOX) {
     int ex, rbt;
-    philox_draw(g, t + (1 << 26), key, 0.5, &ex, &rbt);
+    philox_draw(g, t + (1 << 26), key, 1ull << 52, &ex, &rbt);  // rand < 0.5
     return ex;
   } else {
     return a.draws[(size_t)2 * a.plane + rb + g];
@@ -612,10 +612,13 @@ __device__ __forceinline__ float diag_td(const double (&q)[4], const double (&qb
 
 // TD update of the operator for one agent (algorithms.py:112-341) and the
 // diagnostic TD on the updated table (spgg.py:446-473).  Returns |diag_alpha*td'|.
+// diag = false (kappa == 0: the NI percent it feeds is exactly 0) skips the
+// diagnostic and returns 0.
 template <int ALG, int RNG, typename PT>
 __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size_t rb, int g, int t,
-                                           uint32_t key, double eps, double rew, int so, int act, int sn,
-                                           double (&q)[4], double (&qb)[ALG == ALG_DQ ? 4 : 1]) {
+                                           uint32_t key, double eps, uint64_t eps53, bool diag, double rew,
+                                           int so, int act, int sn, double (&q)[4],
+                                           double (&qb)[ALG == ALG_DQ ? 4 : 1]) {
   const double alpha = pg.alpha, gamma = pg.gamma, dgamma = pg.diag_gamma;
   const int e = so * 2 + act;
   if constexpr (ALG == ALG_DQ) {
@@ -635,7 +638,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     const double nq1 = up1 ? u1 : qc1, nq2 = up1 ? qc2 : u2;
     q[0] = e == 0 ? nq1 : x0; q[1] = e == 1 ? nq1 : x1; q[2] = e == 2 ? nq1 : x2; q[3] = e == 3 ? nq1 : x3;
     qb[0] = e == 0 ? nq2 : y0; qb[1] = e == 1 ? nq2 : y1; qb[2] = e == 2 ? nq2 : y2; qb[3] = e == 3 ? nq2 : y3;
-    return diag_td<ALG>(q, qb, e, sn, rew, pg, eps);
+    return diag ? diag_td<ALG>(q, qb, e, sn, rew, pg, eps) : 0.f;
   } else {
     const double qc = q_get(q, e);
     const double v0 = sn ? q[2] : q[0], v1 = sn ? q[3] : q[1];
@@ -644,7 +647,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
       target = fmax(v0, v1);                                         // algorithms.py:124-127
     } else if constexpr (ALG == ALG_SARSA) {
       int ex, rbt;                                                   // next action, spgg.py:434
-      draw_pair<RNG>(a, rb, g, t, key, eps, 1, &ex, &rbt);
+      draw_pair<RNG>(a, rb, g, t, key, eps53, 1, &ex, &rbt);
       target = (ex ? rbt : greedy2(v0, v1)) ? v1 : v0;               // algorithms.py:168-171
     } else {
       target = expected_q(v0, v1, eps);                              // algorithms.py:205-222
@@ -652,10 +655,11 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     const double td = (rew + gamma * target) - qc;
     const double q1 = qc + alpha * td;
     q_set(q, e, q1);
+    if (!diag) return 0.f;
     if constexpr (ALG == ALG_SARSA) {
       const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];     // updated table
       int ex, rbt;                                                   // diagnostic select, spgg.py:452
-      draw_pair<RNG>(a, rb, g, t, key, eps, 2, &ex, &rbt);
+      draw_pair<RNG>(a, rb, g, t, key, eps53, 2, &ex, &rbt);
       const double target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
       return (float)fabs(pg.diag_alpha * ((rew + dgamma * target2) - q1));
     } else {
@@ -821,6 +825,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
   const double lam_rcp = 1.0 / lam_den;  // IEEE, once per workgroup
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
+  const uint64_t eps53 = u53_threshold(eps_t);  // rand < eps_t as an integer compare
   // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
   const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
                         (uint32_t)pg.stream_id * 0xC2B2AE35u;
@@ -877,15 +882,16 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
         const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
         const int e = pending_entry(b);
-        const float atd = atd_own[u];
-        const double nu = pending_nu(b, md_own[u], kappa, lam_den, lam_rcp);
-        q_set(q[u], e, q_get(q[u], e) + nu);
-        if constexpr (QB) q_set(qb[u], e, q_get(qb[u], e) + nu);  // both tables (spgg.py:496-502)
-        // NI percent (spgg.py:512; x100 applied to the workgroup total): exactly 0
-        // when kappa == 0 (nu = 0), a replica-uniform skip
+        // kappa == 0 (a replica-uniform skip): nu = +0, q + 0 == q (Q never holds -0.0:
+        // U(-0.01,0.01) draws and TD sums of finite values give +0 for exact zeros),
+        // and the NI percent is exactly 0
         if (kappa != 0.0) {
+          const double nu = pending_nu(b, md_own[u], kappa, lam_den, lam_rcp);
+          q_set(q[u], e, q_get(q[u], e) + nu);
+          if constexpr (QB) q_set(qb[u], e, q_get(qb[u], e) + nu);  // both tables (spgg.py:496-502)
+          // NI percent (spgg.py:512; x100 applied to the workgroup total)
           const double anu = fabs(nu);
-          pct = __builtin_fma(anu * rcp_diag(((double)atd + anu) + 1e-8), vmu, pct);
+          pct = __builtin_fma(anu * rcp_diag(((double)atd_own[u] + anu) + 1e-8), vmu, pct);
         }
         const double cm = ((b >> 3) & 1) ? 0.0 : vmu;                  // prev_S of t-1 == C
 #pragma unroll
@@ -935,7 +941,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     if constexpr (AS) so = s_t == 0 ? 1 : 0;
     else so = rep_state_lds<M2>(sR, ca, ly.aw);
     int ex, rbt;                                          // algorithms.py:105-109
-    draw_pair<RNG>(a, rb, gidx[u], t, pkey, eps_t, 0, &ex, &rbt);
+    draw_pair<RNG>(a, rb, gidx[u], t, pkey, eps53, 0, &ex, &rbt);
     double qs0, qs1;
     select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
     const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0
@@ -979,7 +985,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         w0 = rv[j][QB ? 2 : 0];
         w1 = rv[j][QB ? 3 : 0];
       }
-      if (pending) {
+      if (pending && kappa != 0.0) {  // kappa == 0: nu = +0 (see phase 1a)
         const int e = pending_entry(b);
         if ((e >> 1) == ((b >> 4) & 1)) {  // the NI entry lies in the published row
           const double nu = pending_nu(b, rv[j][PF - 1], kappa, lam_den, lam_rcp);
@@ -993,7 +999,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
                                    hp.norm_rcp);
       const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sR[ay * ly.aw + ax]);
       int ex, rbt;
-      draw_pair<RNG>(a, rb, g, t, pkey, eps_t, 0, &ex, &rbt);
+      draw_pair<RNG>(a, rb, g, t, pkey, eps53, 0, &ex, &rbt);
       const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
       const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
       const double rr = act == 0 ? 0.5 : 0.0;
@@ -1020,8 +1026,9 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      const float atd = td_update<ALG, RNG>(a, hp, rb, gidx[u], t, pkey, eps_t, rew, so, act, sn, q[u], qb[u]);
-      a.atd[rb + gidx[u]] = atd;
+      const float atd = td_update<ALG, RNG>(a, hp, rb, gidx[u], t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
+                                            act, sn, q[u], qb[u]);
+      if (kappa != 0.0) a.atd[rb + gidx[u]] = atd;  // read only for the NI percent (0 when kappa == 0)
       store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;

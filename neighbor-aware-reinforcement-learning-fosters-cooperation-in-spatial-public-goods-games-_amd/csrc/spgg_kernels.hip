@@ -47,7 +47,8 @@ using namespace spgg;
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
 //   128 = memory only (the owned loads, staging and stores, no compute),
-//   256 / 512 = Philox / payoff computed twice (value-preserving: marginal-cost probes)
+//   256 / 512 = Philox / payoff computed twice (value-preserving: marginal-cost probes),
+//   1024 = compute only (synthetic inputs instead of the agent loads, no agent stores; TWC kernels)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
@@ -442,7 +443,11 @@ struct RowWindow {
       int gy = y0 + row;
       gy += gy < 0 ? L : 0;
       gy -= gy >= L ? L : 0;
+#if SPGG_ABLATE & 1024
+      buf[j] = (StageReg<T>)((gy * 7 + gx * 3) & 1);
+#else
       buf[j] = src[gy * L + gx];
+#endif
     }
   }
   template <int PITCH>
@@ -759,11 +764,16 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       // first one and drop it): conditional loads serialise on each other
       const int g = own ? (y0 + r) * L + (x0 + c) : y0 * L + x0;
       gidx[u] = g;
+#if SPGG_ABLATE & 1024
+      q[u][0] = 1e-3 * (g & 7); q[u][1] = 1e-3 * ((g >> 3) & 7); q[u][2] = 2e-3; q[u][3] = 1e-3 * (tid & 3);
+      if (pending) { md_own[u] = 0.01 * (g & 3); atd_own[u] = 0.5f; }
+#else
       load_q<QB>(a.Q, rb + g, q[u], qb[u]);
       if (pending) {
         md_own[u] = a.md[rb + g];
         atd_own[u] = a.atd[rb + g];
       }
+#endif
       r += dr;
       c += dc;
       if (c >= tw) {
@@ -779,7 +789,13 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   {
     const int2* rtab = a.ring + (size_t)tile * a.ring_max;
 #pragma unroll
-    for (int j = 0; j < RP; ++j) re[j] = rtab[min(tid + j * kBlock, ring - 1)];
+    for (int j = 0; j < RP; ++j) {
+#if SPGG_ABLATE & 1024
+      re[j] = make_int2(tid + 3 * j, (tid * 7 + j) & 63);
+#else
+      re[j] = rtab[min(tid + j * kBlock, ring - 1)];
+#endif
+    }
   }
   // halo windows into registers (TWC: row-per-wave; rows <= TH + 2*halo, TH <= 25 host-checked)
   constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
@@ -849,7 +865,13 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
 #pragma unroll
     for (int j = 0; j < RP; ++j)
 #pragma unroll
-      for (int f = 0; f < PF; ++f) rv[j][f] = pin[re[j].y + f * a.PB];
+      for (int f = 0; f < PF; ++f) {
+#if SPGG_ABLATE & 1024
+        rv[j][f] = 1e-3 * ((re[j].y + f) & 7);
+#else
+        rv[j][f] = pin[re[j].y + f * a.PB];
+#endif
+      }
   }
   __syncthreads();
   if constexpr (TWC == 0) {  // flattened staging: cooperator rows from the staged bytes
@@ -952,7 +974,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     sA[ca] = (uint8_t)act;
     sRn[ca] = (RT)rn;
     sRew[ca] = rew;
-    Rout[rb + gidx[u]] = (RT)rn;
+    if (!(SPGG_ABLATE & 1024)) Rout[rb + gidx[u]] = (RT)rn;
     own_bits[u] = act | (so << 1) | (s_t << 3);
     cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
     cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
@@ -1014,6 +1036,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
 
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;
+  [[maybe_unused]] double sink = 0.0;  // compute-only probe (SPGG_ABLATE & 1024)
   if (acting) {
     double* pout = a.pub_out + (size_t)(rep * a.tiles_per_rep + tile) * PF * a.PB;
 #pragma unroll
@@ -1028,8 +1051,12 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
       const float atd = td_update<ALG, RNG>(a, hp, rb, gidx[u], t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
                                             act, sn, q[u], qb[u]);
-      if (kappa != 0.0) a.atd[rb + gidx[u]] = atd;  // read only for the NI percent (0 when kappa == 0)
-      store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
+      if (SPGG_ABLATE & 1024) {
+        sink += q[u][0] + q[u][1] + q[u][2] + q[u][3] + (double)atd;
+      } else {
+        if (kappa != 0.0) a.atd[rb + gidx[u]] = atd;  // read only for the NI percent (0 when kappa == 0)
+        store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
+      }
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -1049,9 +1076,13 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = fmax(bmax, mdp);
-      a.md[rb + gidx[u]] = mdp;
-      a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
-      if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
+      if (SPGG_ABLATE & 1024) {
+        sink += mdp + (double)(own_bits[u] | (dp << 2) | (sn << 4));
+      } else {
+        a.md[rb + gidx[u]] = mdp;
+        a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
+      }
+      if (!(SPGG_ABLATE & 1024) && spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + spgg_impl::border_slot(r, c, th, tw, HA);
         rec[0] = sn ? q[u][2] : q[u][0];
         rec[a.PB] = sn ? q[u][3] : q[u][1];
@@ -1124,6 +1155,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);
     }
   }
+  if (SPGG_ABLATE & 1024) bmax += sink * 1e-300;  // keep the probe's results live
   if (acting) {
     __syncthreads();
     const double bm = block_reduce_max(bmax, red);

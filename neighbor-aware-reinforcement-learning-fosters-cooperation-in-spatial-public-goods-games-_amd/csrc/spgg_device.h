@@ -132,19 +132,26 @@ __device__ __forceinline__ double block_reduce(double (&v)[K], double* lds) {
   return tot;
 }
 
-// Max of non-negative v over the workgroup, valid in thread 0.  lds: kWaves doubles.
-__device__ __forceinline__ double block_reduce_max(double v, double* lds) {
-#pragma unroll
-  for (int mask = 32; mask >= 1; mask >>= 1) v = fmax(v, __shfl_xor(v, mask));
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) lds[wave] = v;
-  __syncthreads();
-  double m = 0.0;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) m = fmax(m, lds[w]);
-  }
-  return m;
+// Max over the wave, in every lane: permlane32/16 swaps, then DPP partners
+// l^8, l^7, l^2, l^1 (together they span the 16-lane row), no LDS.
+template <int MASK>
+__device__ __forceinline__ double swap_max(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto l = MASK == 32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                            : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = MASK == 32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                            : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return fmax(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+  v = swap_max<32>(v);
+  v = swap_max<16>(v);
+  v = fmax(v, partner<8>(v));
+  v = fmax(v, partner<4>(v));
+  v = fmax(v, partner<2>(v));
+  v = fmax(v, partner<1>(v));
+  return v;
 }
 
 // ---------------------------------------------------------------------------

@@ -46,9 +46,7 @@ using namespace spgg;
 // Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
-//   128 = memory only (the owned loads, staging and stores, no compute),
-//   256 / 512 = Philox / payoff computed twice (value-preserving: marginal-cost probes),
-//   1024 = compute only (synthetic inputs instead of the agent loads, no agent stores; TWC kernels)
+//   128 = memory only (the owned loads, staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
@@ -160,11 +158,15 @@ constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_A, off_M, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, bytes;
 };
 
+// Pitch of the plus-count plane: one 64-lane wave row per region row.
+constexpr int kPcPitch = 64;
+
 // 16-byte aligned carve: f64 first, then the R planes (rsz = 8 or 1), then bytes.
-// S planes: tile + halo HS (payoffs over tile + HA); everything else tile + HA.
+// S and defector-bit planes: tile + halo HS (payoffs over tile + HA); the
+// plus-count plane: tile + HA + 1 rows of kPcPitch; everything else tile + HA.
 __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, int rsz) {
   LdsLayout l;
   l.sw = tw + 2 * HS; l.sh = th + 2 * HS;
@@ -175,23 +177,22 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_R = off;    off += ((na * rsz + 15) / 16) * 16;
   l.off_Rn = off;   off += ((na * rsz + 15) / 16) * 16;
   l.off_S = off;    off += ((l.sw * l.sh + 15) / 16) * 16;
+  l.off_D = off;    off += ((l.sw * l.sh + kPcPitch + 15) / 16) * 16;  // + slack: full-wave row reads
   l.off_A = off;    off += ((na + 15) / 16) * 16;
-  l.off_M = off;    off += ((l.sh * 3 * 4 + 15) / 16) * 16;  // cooperator bitmask rows (3 dwords)
+  l.off_PC = off;   off += (l.ah + 2) * kPcPitch;
   l.bytes = off;
   return l;
 }
 
-// Cooperator indicators of the 13 cells around centre index c of a byte grid
-// with row pitch w (bit0 = strategy, 0 = cooperate).
-__device__ __forceinline__ Cells13 cells_at(const uint8_t* s, int c, int w) {
-#define CO(o) ((s[c + (o)] & 1) ? 0 : 1)
-  Cells13 r;
-  r.c00 = CO(0);
-  r.cm0 = CO(-w); r.cp0 = CO(w); r.c0m = CO(-1); r.c0p = CO(1);
-  r.cmm = CO(-w - 1); r.cmp = CO(-w + 1); r.cpm = CO(w - 1); r.cpp = CO(w + 1);
-  r.cM0 = CO(-2 * w); r.cP0 = CO(2 * w); r.c0M = CO(-2); r.c0P = CO(2);
-#undef CO
-  return r;
+// Element i of a per-replica array: scalar base + zero-extended 32-bit byte
+// offset, so every access is one global_load/store in saddr form with no
+// 64-bit address arithmetic (the host keeps each per-replica array < 4 GiB).
+// (char-pointer arithmetic, not an integer round trip: the compiler must still
+// see a global pointer, or it falls back to flat instructions.)
+template <typename T>
+__device__ __forceinline__ T* at(T* base, uint32_t i) {
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + (size_t)(i * (uint32_t)sizeof(T)));
 }
 
 // Compact reputation: when rep_gain_C, delta_R_D, R_min, R_max are multiples
@@ -203,9 +204,9 @@ using RStore = typename std::conditional<RQ, int8_t, double>::type;
 template <bool RQ>
 using RVal = typename std::conditional<RQ, int, double>::type;
 
-// The per-agent fields of spgg_rep_params, copied to registers once per
-// workgroup (read through a reference into global memory the compiler must
-// assume the agents' stores may alias them and reloads them per agent).
+// The per-agent fields of spgg_rep_params, copied to LDS once per workgroup
+// (read through a reference into global memory the compiler must assume the
+// agents' stores may alias them and reloads them per agent).
 struct HotParams {
   double norm_min, norm_den, norm_rcp, alpha, gamma, diag_alpha, diag_gamma;
   double rep_gain_c, neg_delta_r_d, r_min, r_max;
@@ -289,19 +290,19 @@ __device__ __forceinline__ int wrap1(int x, int L, bool tiny) {
   return x;
 }
 
-// Copy an h x w window of a periodic L x L plane (origin y0, x0; may wrap)
-// into LDS, flattened over all 256 threads.  Every global load of the thread
-// is issued before the first LDS store: one memory round trip
-// (J >= h*w/kBlock; host-checked).  Measured 5% faster than one-row-per-wave
-// staging (lane-constant columns but 28% idle lanes at 46-wide rows).
 // Register type of a staged element: sub-dword values are held one per VGPR
 // (packing bytes with v_perm would make every load wait for the previous one).
 template <typename T>
 using StageReg = typename std::conditional<(sizeof(T) < 4), int, T>::type;
 
+// Copy an h x w window of a periodic L x L plane (origin y0, x0; may wrap)
+// into LDS, flattened over all threads (tiles of run-time width).  Every
+// global load of the thread is issued before the first LDS store: one memory
+// round trip (J >= h*w/kBlock; host-checked).  dbit (S windows): also the
+// defector-bit plane (bit0 of each byte) at the same pitch.
 template <int J, typename T>
 __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, int h, int w, int y0, int x0,
-                                             int L, bool tiny) {
+                                             int L, bool tiny, uint8_t* dbit = nullptr) {
   const int total = h * w;
   const int tid = threadIdx.x;
   const int dr = kBlock / w, dc = kBlock - (kBlock / w) * w;
@@ -313,7 +314,7 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
     di[j] = r * pitch + c;
     // unconditional load (tail rows clamped into the window): conditional loads
     // make the compiler wait on each one before the next is issued
-    buf[j] = src[wrap1(y0 + min(r, h - 1), L, tiny) * L + wrap1(x0 + c, L, tiny)];
+    buf[j] = *at(src, (uint32_t)(wrap1(y0 + min(r, h - 1), L, tiny) * L + wrap1(x0 + c, L, tiny)));
     r += dr;
     c += dc;
     if (c >= w) {
@@ -323,110 +324,19 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
   }
 #pragma unroll
   for (int j = 0; j < J; ++j)
-    if (tid + j * kBlock < total) dst[di[j]] = (T)buf[j];
-}
-
-// Row-per-wave variant for a compile-time window width W <= 64 (TWC kernels,
-// L >= 2W): wave w copies rows w, w+4, ...; the row index and its wrap are
-// wave-uniform (scalar ALU), the column wrap is computed once per lane, so a
-// row costs ~3 vector instructions instead of ~30 for the flattened walk.
-template <int J, int W, int PITCH, typename T>
-__device__ __forceinline__ void stage_rows(T* dst, const T* src, int h, int y0, int x0, int L,
-                                           uint32_t* coop_rows = nullptr) {
-  static_assert(W <= 64, "one row per wave instruction");
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool in_row = lane < W;
-  int gx = x0 + (in_row ? lane : W - 1);
-  gx += gx < 0 ? L : 0;
-  gx -= gx >= L ? L : 0;
-  StageReg<T> buf[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {  // unconditional loads (rows clamped): one round trip
-    const int row = min(wave + j * kWaves, h - 1);
-    int gy = y0 + row;
-    gy += gy < 0 ? L : 0;
-    gy -= gy >= L ? L : 0;
-    buf[j] = src[gy * L + gx];
-  }
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int row = wave + j * kWaves;
-    if (in_row && row < h) dst[row * PITCH + lane] = (T)buf[j];
-    if constexpr (sizeof(T) == 1) {
-      if (coop_rows && row < h) {  // bit x = cooperator at window column x (S bit0 == 0)
-        const uint64_t m = __ballot(in_row && !(buf[j] & 1));
-        if (lane == 0) {
-          coop_rows[row * 3] = (uint32_t)m;
-          coop_rows[row * 3 + 1] = (uint32_t)(m >> 32);
-          coop_rows[row * 3 + 2] = 0u;
-        }
+    if (tid + j * kBlock < total) {
+      dst[di[j]] = (T)buf[j];
+      if constexpr (sizeof(T) == 1) {
+        if (dbit) dbit[di[j]] = (uint8_t)(buf[j] & 1);
       }
     }
-  }
 }
 
-// The same cooperator bitmask rows from an h x w byte window already in LDS
-// (flattened-staging path; w <= 64).
-__device__ __forceinline__ void coop_rows_from_lds(uint32_t* coop_rows, const uint8_t* s, int pitch, int h, int w) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int row = wave; row < h; row += kWaves) {
-    const bool in_row = lane < w;
-    const uint64_t m = __ballot(in_row && !(s[row * pitch + (in_row ? lane : 0)] & 1));
-    if (lane == 0) {
-      coop_rows[row * 3] = (uint32_t)m;
-      coop_rows[row * 3 + 1] = (uint32_t)(m >> 32);
-      coop_rows[row * 3 + 2] = 0u;
-    }
-  }
-}
-
-// Payoff of the agent at window row ry, column cx from the cooperator
-// bitmask rows (spgg.py:230-259, 373-377): the 5-cell windows of rows
-// ry-2..ry+2 packed into one 25-bit word X, each group count N_k one
-// popcount of X under a constant mask; then the reference's table sum.
-__device__ __forceinline__ double payoff_rows_(const uint32_t* M, int ry, int cx, const double* tab,
-                                               double norm_min, double norm_den, double norm_rcp);
-__device__ __forceinline__ double payoff_rows(const uint32_t* M, int ry, int cx, const double* tab,
-                                              double norm_min, double norm_den, double norm_rcp) {
-#if SPGG_ABLATE & 512
-  int ry2 = ry;
-  asm volatile("" : "+v"(ry2));
-  return (payoff_rows_(M, ry, cx, tab, norm_min, norm_den, norm_rcp) +
-          payoff_rows_(M, ry2, cx, tab, norm_min, norm_den, norm_rcp)) * 0.5;
-#else
-  return payoff_rows_(M, ry, cx, tab, norm_min, norm_den, norm_rcp);
-#endif
-}
-__device__ __forceinline__ double payoff_rows_(const uint32_t* M, int ry, int cx, const double* tab,
-                                               double norm_min, double norm_den, double norm_rcp) {
-  const int s = cx - 2, sw = s >> 5, sb = s & 31;
-  const uint32_t* m = M + (ry - 2) * 3 + sw;
-  uint32_t X = 0;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {  // row ry-2+k -> bits 5k..5k+4 (column cx-2+i -> bit i)
-    const uint32_t win = __builtin_amdgcn_alignbit(m[k * 3 + 1], m[k * 3], sb) & 31u;
-    X |= win << (5 * k);
-  }
-  constexpr uint32_t C = 0x4u;  // centre column bit of a 5-bit row window
-  constexpr uint32_t MN0 = (0xEu << 10) | (C << 5) | (C << 15);      // group (0,0)
-  constexpr uint32_t MN1 = (0xEu << 5) | C | (C << 10);              // group (1,0): centred at row -1
-  constexpr uint32_t MN2 = (0xEu << 15) | (C << 10) | (C << 20);     // group (-1,0): row +1
-  constexpr uint32_t MN3 = (0x7u << 10) | (0x2u << 5) | (0x2u << 15); // group (1,1): column -1
-  constexpr uint32_t MN4 = (0x1Cu << 10) | (0x8u << 5) | (0x8u << 15); // group (-1,1): column +1
-  const int c00 = (X >> 12) & 1;
-  const double* tb = tab + (c00 ? 0 : 6);
-  double tot = tb[__builtin_popcount(X & MN0)];
-  tot = tot + tb[__builtin_popcount(X & MN1)];
-  tot = tot + tb[__builtin_popcount(X & MN2)];
-  tot = tot + tb[__builtin_popcount(X & MN3)];
-  tot = tot + tb[__builtin_popcount(X & MN4)];
-  return div_uniform(tot - norm_min, norm_den, norm_rcp);  // (tot - (r-5)) / (4r - (r-5))
-}
-
-// Split form of stage_rows: load() issues the window's loads into registers,
-// store() (later, after other loads were issued) writes them to LDS.
+// Row-per-wave window for a compile-time width W <= 64 (TWC kernels, L >= 2W):
+// wave w holds rows w, w+4, ...; the row index and its wrap are wave-uniform
+// (scalar ALU), the column wrap is computed once per lane.  load() issues the
+// window's loads into registers, store() (later, after other loads were
+// issued) writes them to LDS -- for S windows also the defector-bit plane.
 template <int J, int W, typename T>
 struct RowWindow {
   StageReg<T> buf[J];
@@ -443,43 +353,59 @@ struct RowWindow {
       int gy = y0 + row;
       gy += gy < 0 ? L : 0;
       gy -= gy >= L ? L : 0;
-#if SPGG_ABLATE & 1024
-      buf[j] = (StageReg<T>)((gy * 7 + gx * 3) & 1);
-#else
-      buf[j] = src[gy * L + gx];
-#endif
+      buf[j] = *at(src, (uint32_t)(gy * L + gx));
     }
   }
   template <int PITCH>
-  __device__ __forceinline__ void store(T* dst, int h, uint32_t* coop_rows) {
+  __device__ __forceinline__ void store(T* dst, int h, uint8_t* dbit) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool in_row = lane < W;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int row = wave + j * kWaves;
-      if (in_row && row < h) dst[row * PITCH + lane] = (T)buf[j];
-      if constexpr (sizeof(T) == 1) {
-        if (coop_rows && row < h) {  // bit x = cooperator at window column x (S bit0 == 0)
-          const uint64_t m = __ballot(in_row && !(buf[j] & 1));
-          if (lane == 0) {
-            coop_rows[row * 3] = (uint32_t)m;
-            coop_rows[row * 3 + 1] = (uint32_t)(m >> 32);
-            coop_rows[row * 3 + 2] = 0u;
-          }
+      if (in_row && row < h) {
+        dst[row * PITCH + lane] = (T)buf[j];
+        if constexpr (sizeof(T) == 1) {
+          if (dbit) dbit[row * PITCH + lane] = (uint8_t)(buf[j] & 1);
         }
       }
     }
   }
 };
 
-// Stage an h x w window: row-per-wave when the width is a compile-time
-// constant (TWC), else the flattened walk.
-template <int TWC, int HALO, int JF, int JR, typename T>
-__device__ __forceinline__ void stage(T* dst, int pitch, const T* src, int h, int w, int y0, int x0, int L,
-                                      bool tiny, uint32_t* coop_rows = nullptr) {
-  if constexpr (TWC > 0) stage_rows<JR, TWC + 2 * HALO, TWC + 2 * HALO>(dst, src, h, y0, x0, L, coop_rows);
-  else stage_region<JF>(dst, pitch, src, h, w, y0, x0, L, tiny);
+// Plus-shaped defector counts over the region + 1 ring, x8 (byte offsets into
+// a payoff table indexed by defector count): pc[(y)*64 + x] for region cell
+// (y - 1, x - 1) = defector bits of S-window cells (y+1, x+1) and its four
+// neighbours.  One wave row per region row; lanes past the row width compute
+// unused cells (the D plane carries read slack).
+__device__ __forceinline__ void build_plus_counts(uint8_t* pc, const uint8_t* d, int sw, int rows) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int y = wave; y < rows; y += kWaves) {
+    const uint8_t* p = d + y * sw + lane;
+    const int cnt = p[1] + p[sw] + p[sw + 1] + p[sw + 2] + p[2 * sw + 1];
+    pc[y * kPcPitch + lane] = (uint8_t)(cnt << 3);
+  }
+}
+
+// Payoff of the region cell (ry, rx) (spgg.py:230-259, 373-377): the five
+// group defector counts are plus counts at the cell and its four axial
+// neighbours, each a byte offset into tb = the table of the cell's own
+// strategy indexed by defector count; summed in the reference's group order,
+// normalised.
+__device__ __forceinline__ double payoff_pc(const uint8_t* pc, int ry, int rx, const double* tb, double norm_min,
+                                            double norm_den, double norm_rcp) {
+  const uint8_t* p = pc + ry * kPcPitch + rx + 1;  // plus count of N0[i-1, j]
+  const char* t = reinterpret_cast<const char*>(tb);
+#define T_AT(o) (*reinterpret_cast<const double*>(t + (o)))
+  double tot = T_AT(p[kPcPitch]);             // group (0,0)  -> N0[i,j]
+  tot = tot + T_AT(p[0]);                      // group (1,0)  -> N0[i-1,j]
+  tot = tot + T_AT(p[2 * kPcPitch]);           // group (-1,0) -> N0[i+1,j]
+  tot = tot + T_AT(p[kPcPitch - 1]);           // group (1,1)  -> N0[i,j-1]
+  tot = tot + T_AT(p[kPcPitch + 1]);           // group (-1,1) -> N0[i,j+1]
+#undef T_AT
+  return div_uniform(tot - norm_min, norm_den, norm_rcp);  // (tot - (r-5)) / (4r - (r-5))
 }
 
 // 1/x to full f64 precision for DIAGNOSTIC quotients only (history values,
@@ -494,7 +420,8 @@ __device__ __forceinline__ double rcp_diag(double x) {
 // History counters as 16-bit fields f = 0..10, two per dword (word f>>1,
 // half f&1; a workgroup counts at most 1024 agents, so fields never carry):
 //   SW_CD, SW_DC, NCOOP, NMD_POS, NMD_POS2, GC0, GC1, ..., GC5.
-// Words 2-3 and 4-5 are accumulated as 64-bit pairs (fields 4-7, 8-11).
+// Per thread the group-composition counts GC0..5 are nibbles of one word
+// (<= APT agents each) until they are spread into the fields.
 
 // Q table helpers.  QB = 1 for Double Q-learning (second table qb), else the
 // qb arrays are dead and the compiler drops them.
@@ -529,14 +456,6 @@ __device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, i
     *ex = ((g * 2654435761u + t + k) >> 7) % 50 == 0; *rbt = (g ^ t ^ k) & 1;
 #else
     philox_draw(g, t + (k << 26), key, thr, ex, rbt);
-#if SPGG_ABLATE & 256
-    int g2 = g;
-    asm volatile("" : "+v"(g2));
-    int ex2, rbt2;
-    philox_draw(g2, t + (k << 26), key, thr, &ex2, &rbt2);
-    *ex = *ex & ex2;
-    *rbt = *rbt & rbt2;
-#endif
 #endif
   } else {
     *ex = a.draws[(size_t)(2 * k) * a.plane + rb + g];
@@ -557,8 +476,9 @@ __device__ __forceinline__ int draw_table1(const TileArgs& a, size_t rb, int g, 
 }
 
 template <int QB>
-__device__ __forceinline__ void load_q(const double* Q, size_t agent, double (&q)[4], double (&qb)[QB ? 4 : 1]) {
-  const double2* qp = reinterpret_cast<const double2*>(Q + agent * (QB ? 8 : 4));
+__device__ __forceinline__ void load_q(const double* Qr, uint32_t agent, double (&q)[4],
+                                       double (&qb)[QB ? 4 : 1]) {
+  const double2* qp = at(reinterpret_cast<const double2*>(Qr), agent * (QB ? 4 : 2));
   const double2 q01 = qp[0], q23 = qp[1];
   q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
   if constexpr (QB) {
@@ -568,9 +488,9 @@ __device__ __forceinline__ void load_q(const double* Q, size_t agent, double (&q
 }
 
 template <int QB>
-__device__ __forceinline__ void store_q(double* Q, size_t agent, const double (&q)[4],
+__device__ __forceinline__ void store_q(double* Qr, uint32_t agent, const double (&q)[4],
                                         const double (&qb)[QB ? 4 : 1]) {
-  double2* qo = reinterpret_cast<double2*>(Q + agent * (QB ? 8 : 4));
+  double2* qo = at(reinterpret_cast<double2*>(Qr), agent * (QB ? 4 : 2));
   qo[0] = make_double2(q[0], q[1]);
   qo[1] = make_double2(q[2], q[3]);
   if constexpr (QB) {
@@ -594,24 +514,15 @@ __device__ __forceinline__ void select_row(const double (&q)[4], const double (&
   }
 }
 
-// Diagnostic TD on the UPDATED table (spgg.py:446-473) for every operator but
-// SARSA (whose diagnostic target is a fresh eps-greedy draw): |diag_alpha*td'|
-// with e = (s_old, a) and sn the new state.  Used right after the TD update
-// and again, on the same stored table, when the next launch recomputes it.
-template <int ALG, typename PT>
-__device__ __forceinline__ float diag_td(const double (&q)[4], const double (&qb)[ALG == ALG_DQ ? 4 : 1], int e,
-                                         int sn, double rew, const PT& pg, double eps) {
-  double td2;
-  if constexpr (ALG == ALG_DQ) {  // on the mean table (spgg.py:463-467)
-    const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
-    const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
-    const double m0 = sn ? m10 : m00, m1 = sn ? m11 : m01;
-    td2 = (rew + pg.diag_gamma * fmax(m0, m1)) - mean2(q_get(q, e), q_get(qb, e));
-  } else {
-    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];
-    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps) : fmax(w0, w1);
-    td2 = (rew + pg.diag_gamma * target2) - q_get(q, e);
-  }
+// Diagnostic TD on the UPDATED table (spgg.py:446-473), Double-Q: on the mean
+// table, |diag_alpha*td'| with e = (s_old, a) and sn the new state.
+template <typename PT>
+__device__ __forceinline__ float diag_td_dq(const double (&q)[4], const double (&qb)[4], int e, int sn, double rew,
+                                            const PT& pg) {
+  const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
+  const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
+  const double m0 = sn ? m10 : m00, m1 = sn ? m11 : m01;
+  const double td2 = (rew + pg.diag_gamma * fmax(m0, m1)) - mean2(q_get(q, e), q_get(qb, e));
   return (float)fabs(pg.diag_alpha * td2);
 }
 
@@ -643,10 +554,12 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     const double nq1 = up1 ? u1 : qc1, nq2 = up1 ? qc2 : u2;
     q[0] = e == 0 ? nq1 : x0; q[1] = e == 1 ? nq1 : x1; q[2] = e == 2 ? nq1 : x2; q[3] = e == 3 ? nq1 : x3;
     qb[0] = e == 0 ? nq2 : y0; qb[1] = e == 1 ? nq2 : y1; qb[2] = e == 2 ? nq2 : y2; qb[3] = e == 3 ? nq2 : y3;
-    return diag ? diag_td<ALG>(q, qb, e, sn, rew, pg, eps) : 0.f;
+    return diag ? diag_td_dq(q, qb, e, sn, rew, pg) : 0.f;
   } else {
-    const double qc = q_get(q, e);
+    // rows of the old and the new state; the updated entry is (so, act)
+    const double o0 = so ? q[2] : q[0], o1 = so ? q[3] : q[1];
     const double v0 = sn ? q[2] : q[0], v1 = sn ? q[3] : q[1];
+    const double qc = act ? o1 : o0;
     double target;
     if constexpr (ALG == ALG_Q) {
       target = fmax(v0, v1);                                         // algorithms.py:124-127
@@ -659,17 +572,19 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     }
     const double td = (rew + gamma * target) - qc;
     const double q1 = qc + alpha * td;
-    q_set(q, e, q1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = e == k ? q1 : q[k];
     if (!diag) return 0.f;
+    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];       // updated table, row s'
+    double target2;
     if constexpr (ALG == ALG_SARSA) {
-      const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];     // updated table
       int ex, rbt;                                                   // diagnostic select, spgg.py:452
       draw_pair<RNG>(a, rb, g, t, key, eps53, 2, &ex, &rbt);
-      const double target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
-      return (float)fabs(pg.diag_alpha * ((rew + dgamma * target2) - q1));
+      target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
     } else {
-      return diag_td<ALG>(q, qb, e, sn, rew, pg, eps);
+      target2 = ALG == ALG_ES ? expected_q(w0, w1, eps) : fmax(w0, w1);
     }
+    return (float)fabs(pg.diag_alpha * ((rew + dgamma * target2) - q1));  // Q'[s,a] = q1
   }
 }
 
@@ -684,16 +599,49 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
 // agent-step HBM/Infinity-Cache traffic: Q 32 B read + 32 B written, md 8 + 8,
 // atd 4 + 4, S/R ~5 B, border records ~6 B; the working set of cfg3 (~235 MB)
 // stays within the 256 MB Infinity Cache (a ping-ponged Q alone was 270 MB).
-template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
-// Occupancy floor (waves per SIMD), build knob for A/B timing.
-#ifndef SPGG_MIN_WAVES
-#define SPGG_MIN_WAVES 1
+//
+// Diagnostic build (-DSPGG_STAMPS=1, one stream): workgroups stamp s_memrealtime
+// (100 MHz) at phase boundaries of iteration SPGG_STAMP_T into spgg_stamps
+// [logical][10] (slots 8, 9: HW_ID, XCC_ID); read by spgg_stamps_read.
+#ifndef SPGG_STAMPS
+#define SPGG_STAMPS 0
 #endif
-__global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileArgs a, int t, int fin_only) {
+#if SPGG_STAMPS
+#ifndef SPGG_STAMP_T
+#define SPGG_STAMP_T 30
+#endif
+constexpr int kStampWG = 8192;
+__device__ unsigned long long spgg_stamps[kStampWG * 10];
+#define STAMP(k)                                                                            \
+  do {                                                                                      \
+    if (t == SPGG_STAMP_T && tid == 0 && logical < kStampWG)                                \
+      spgg_stamps[logical * 10 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+//
+// Occupancy floor (waves per SIMD): 4 (<= 128 VGPRs) where that allocates
+// without spilling (first-order Philox kernels of compile-time width, the
+// bench path); elsewhere the compiler's choice.  SPGG_MIN_WAVES overrides.
+constexpr int min_waves(bool m2, int rng, int twc, int alg) {
+#ifdef SPGG_MIN_WAVES
+  return SPGG_MIN_WAVES;
+#else
+  return (!m2 && rng == SPGG_RNG_PHILOX && twc > 0 && alg != SPGG_ALG_DOUBLE_Q) ? 4 : 1;
+#endif
+}
+
+template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
+__global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_step_kernel(TileArgs a, int t,
+                                                                                         int fin_only) {
   using RT = RStore<RQ>;
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
   constexpr int HS = HA + 2;      // S halo: payoffs over tile + HA
   constexpr int QB = ALG == ALG_DQ ? 1 : 0;
+  constexpr int QW = QB ? 8 : 4;
   constexpr int PF = spgg_impl::pf_of(ALG);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -721,15 +669,32 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   double* sRew = reinterpret_cast<double*>(smem + ly.off_Rew);
   RT* sR = reinterpret_cast<RT*>(smem + ly.off_R);
   RT* sRn = reinterpret_cast<RT*>(smem + ly.off_Rn);
-  const RT* Rin = reinterpret_cast<const RT*>(a.R_in);
-  RT* Rout = reinterpret_cast<RT*>(a.R_out);
   uint8_t* sS = smem + ly.off_S;
+  uint8_t* sD = smem + ly.off_D;
   uint8_t* sA = smem + ly.off_A;
-  uint32_t* sM = reinterpret_cast<uint32_t*>(smem + ly.off_M);
-  const bool pending = t > 1;
+  uint8_t* sPC = smem + ly.off_PC;
+  // this replica's arrays: scalar bases, 32-bit element offsets (at())
   const size_t rb = (size_t)rep * n;
+  double* Qr = a.Q + rb * QW;
+  double* mdr = a.md + rb;
+  float* atdr = a.atd + rb;
+  const uint8_t* Sin = a.S_in + rb;
+  uint8_t* Sout = a.S_out + rb;
+  const RT* Rin = reinterpret_cast<const RT*>(a.R_in) + rb;
+  RT* Rout = reinterpret_cast<RT*>(a.R_out) + rb;
+  const bool pending = t > 1;
   const int tid = threadIdx.x;
   const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
+  STAMP(0);
+#if SPGG_STAMPS
+  if (t == SPGG_STAMP_T && tid == 0 && logical < kStampWG) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    spgg_stamps[logical * 10 + 8] = hw;
+    spgg_stamps[logical * 10 + 9] = xcc;
+  }
+#endif
 
   // ---- phase 0: every vector load first, then the replica's state ---------
   // None of these loads depends on the replica's state, so they are all in
@@ -740,13 +705,15 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   // tile's first agent (same inputs, so every value it computes and stores is
   // bit-identical to the owner's); only its history contributions are masked
   // (vm = 0).  Per-slot branches cost more in exec-mask and copy instructions.
-  int gidx[APT], rc[APT];
+  int rc[APT];  // (r << 16) | c of slot u; its agent index is agent_of(rc[u]) (recomputed, not held)
   unsigned vbits = 0;  // bit u: slot u holds an owned agent
   double q[APT][4];
   double qb[APT][QB ? 4 : 1];
   double md_own[APT];
   float atd_own[APT];
   const int n_own = th * tw;
+  const uint32_t g00 = (uint32_t)(y0 * L + x0);
+  auto agent_of = [&](int rcu) { return g00 + (uint32_t)((rcu >> 16) * L + (rcu & 0xffff)); };
   {
     const int dr = kBlock / tw, dc = kBlock - (kBlock / tw) * tw;
     int r = tid / tw, c = tid - (tid / tw) * tw;
@@ -756,24 +723,13 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       const bool own = k < n_own;
       rc[u] = own ? (r << 16) | c : 0;
       vbits |= own ? 1u << u : 0u;
-      md_own[u] = 0.0;
-      atd_own[u] = 0.f;
-      q[u][0] = q[u][1] = q[u][2] = q[u][3] = 0.0;
-      if constexpr (QB) qb[u][0] = qb[u][1] = qb[u][2] = qb[u][3] = 0.0;
       // loads unconditional (threads without a u-th agent read the tile's
-      // first one and drop it): conditional loads serialise on each other
-      const int g = own ? (y0 + r) * L + (x0 + c) : y0 * L + x0;
-      gidx[u] = g;
-#if SPGG_ABLATE & 1024
-      q[u][0] = 1e-3 * (g & 7); q[u][1] = 1e-3 * ((g >> 3) & 7); q[u][2] = 2e-3; q[u][3] = 1e-3 * (tid & 3);
-      if (pending) { md_own[u] = 0.01 * (g & 3); atd_own[u] = 0.5f; }
-#else
-      load_q<QB>(a.Q, rb + g, q[u], qb[u]);
-      if (pending) {
-        md_own[u] = a.md[rb + g];
-        atd_own[u] = a.atd[rb + g];
-      }
-#endif
+      // first one and drop it; md/atd are read even at t = 1, unused there):
+      // conditional loads serialise on each other
+      const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0);
+      load_q<QB>(Qr, g, q[u], qb[u]);
+      md_own[u] = *at(mdr, g);
+      atd_own[u] = *at(atdr, g);
       r += dr;
       c += dc;
       if (c >= tw) {
@@ -789,13 +745,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   {
     const int2* rtab = a.ring + (size_t)tile * a.ring_max;
 #pragma unroll
-    for (int j = 0; j < RP; ++j) {
-#if SPGG_ABLATE & 1024
-      re[j] = make_int2(tid + 3 * j, (tid * 7 + j) & 63);
-#else
-      re[j] = rtab[min(tid + j * kBlock, ring - 1)];
-#endif
-    }
+    for (int j = 0; j < RP; ++j) re[j] = *at(rtab, (uint32_t)min(tid + j * kBlock, ring - 1));
   }
   // halo windows into registers (TWC: row-per-wave; rows <= TH + 2*halo, TH <= 25 host-checked)
   constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
@@ -803,31 +753,22 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
   RowWindow<JSR, TWC + 2 * HS, uint8_t> winS;
   RowWindow<JRR, TWC + 2 * HA, RT> winR;
   if constexpr (TWC > 0) {
-    winS.load(a.S_in + rb, th + 2 * HS, y0 - HS, x0 - HS, L);
-    if (!AS) winR.load(Rin + rb, ah, y0 - HA, x0 - HA, L);
+    winS.load(Sin, th + 2 * HS, y0 - HS, x0 - HS, L);
+    if (!AS) winR.load(Rin, ah, y0 - HA, x0 - HA, L);
   }
 
   // replica state (scalar loads)
   const int st = a.stop_iter[rep];
   const bool dead = st != 0 && st < t;  // absorbed before t: nothing to do
   const spgg_rep_params& pg = a.params[rep];
-#ifndef SPGG_HOT_LDS  // placement knob (A/B: 1 LDS 77.9, 0 registers 79.4, 2 global 80.6 us cfg3)
-#define SPGG_HOT_LDS 1
-#endif
-#if SPGG_HOT_LDS == 1  // per-agent fields in LDS (written before the staging barrier)
-  __shared__ HotParams hps;
+  __shared__ HotParams hps;  // per-agent fields in LDS (written before the staging barrier)
   if (tid == 0) hps = hot_params(pg);
   const HotParams& hp = hps;
-#elif SPGG_HOT_LDS == 2  // read through the global reference
-  const spgg_rep_params& hp = pg;
-#else
-  const HotParams hp = hot_params(pg);
-#endif
-  if (tid == 0) {  // scalar loads of the replica's payoff table (no vector-memory wait)
+  if (tid == 0) {  // scalar loads of the replica's payoff tables, indexed by defector count
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      tab[k] = pg.pay_c[k];
-      tab[6 + k] = pg.pay_d[k];
+      tab[k] = pg.pay_c[5 - k];
+      tab[6 + k] = pg.pay_d[5 - k];
     }
   }
   const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
@@ -848,11 +789,11 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
 
   // windows -> LDS (waits for the loads above)
   if constexpr (TWC > 0) {
-    winS.template store<TWC + 2 * HS>(sS, th + 2 * HS, sM);
+    winS.template store<TWC + 2 * HS>(sS, th + 2 * HS, sD);
     if (!AS) winR.template store<TWC + 2 * HA>(sR, ah, nullptr);
   } else {
-    stage_region<JSF>(sS, ly.sw, a.S_in + rb, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny);
-    if (!AS) stage_region<JRF>(sR, ly.aw, Rin + rb, ah, aw, y0 - HA, x0 - HA, L, tiny);
+    stage_region<JSF>(sS, ly.sw, Sin, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny, sD);
+    if (!AS) stage_region<JRF>(sR, ly.aw, Rin, ah, aw, y0 - HA, x0 - HA, L, tiny);
   }
   if (dead) return;  // workgroup-uniform; no vector load is outstanding here
   if (stop_now && tile == 0 && tid == 0) a.stop_iter[rep] = t;
@@ -865,36 +806,30 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
 #pragma unroll
     for (int j = 0; j < RP; ++j)
 #pragma unroll
-      for (int f = 0; f < PF; ++f) {
-#if SPGG_ABLATE & 1024
-        rv[j][f] = 1e-3 * ((re[j].y + f) & 7);
-#else
-        rv[j][f] = pin[re[j].y + f * a.PB];
-#endif
-      }
+      for (int f = 0; f < PF; ++f) rv[j][f] = *at(pin, (uint32_t)(re[j].y + f * a.PB));
   }
   __syncthreads();
-  if constexpr (TWC == 0) {  // flattened staging: cooperator rows from the staged bytes
-    coop_rows_from_lds(sM, sS, ly.sw, th + 2 * HS, tw + 2 * HS);
-    __syncthreads();
-  }
+  STAMP(1);
   if (SPGG_ABLATE & 128) {  // memory floor: write back what was read
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = rc[u] & 0xffff;
-      store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
-      a.md[rb + gidx[u]] = md_own[u];
-      a.atd[rb + gidx[u]] = atd_own[u];
-      a.S_out[rb + gidx[u]] = sS[(r + HS) * ly.sw + (c + HS)];
-      if (!AS) Rout[rb + gidx[u]] = sR[(r + HA) * ly.aw + (c + HA)];
+      store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
+      *at(mdr, agent_of(rc[u])) = md_own[u];
+      *at(atdr, agent_of(rc[u])) = atd_own[u];
+      *at(Sout, agent_of(rc[u])) = sS[(r + HS) * ly.sw + (c + HS)];
+      if (!AS) *at(Rout, agent_of(rc[u])) = sR[(r + HA) * ly.aw + (c + HA)];
     }
     return;
   }
+  // plus counts for the payoffs of phases 1b / 1c (their barrier: after phase 1a)
+  if (!fin_only) build_plus_counts(sPC, sD, ly.sw, ah + 2);
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
   // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C, 8 NI percent
   {
-    double v[8], pct = 0.0;
+    double v[8];
+    float pct = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.0;
     if (pending) {
@@ -909,11 +844,17 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         // and the NI percent is exactly 0
         if (kappa != 0.0) {
           const double nu = pending_nu(b, md_own[u], kappa, lam_den, lam_rcp);
-          q_set(q[u], e, q_get(q[u], e) + nu);
-          if constexpr (QB) q_set(qb[u], e, q_get(qb[u], e) + nu);  // both tables (spgg.py:496-502)
-          // NI percent (spgg.py:512; x100 applied to the workgroup total)
-          const double anu = fabs(nu);
-          pct = __builtin_fma(anu * rcp_diag(((double)atd_own[u] + anu) + 1e-8), vmu, pct);
+          // Q[s,a] += nu as exact masked FMAs: fma(1, nu, x) = x + nu, fma(0, nu, x) = x
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const double m = e == k ? 1.0 : 0.0;
+            q[u][k] = __builtin_fma(m, nu, q[u][k]);
+            if constexpr (QB) qb[u][k] = __builtin_fma(m, nu, qb[u][QB ? k : 0]);  // both tables (spgg.py:496-502)
+          }
+          // NI percent (spgg.py:512; x100 applied to the workgroup total), in f32:
+          // a history mean (tolerance 1e-5), each term a ratio in [0, 1]
+          const float anu = fabsf((float)nu);
+          pct = __builtin_fmaf(anu * __builtin_amdgcn_rcpf((atd_own[u] + anu) + 1e-8f), (float)vmu, pct);
         }
         const double cm = ((b >> 3) & 1) ? 0.0 : vmu;                  // prev_S of t-1 == C
 #pragma unroll
@@ -925,68 +866,75 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       }
     }
     wave_partials<8>(v, red, 0);
-    double pv[1] = {pct};
+    double pv[1] = {(double)pct};
     wave_partials<1>(pv, red, 8);
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
-    for (int u = 0; u < APT; ++u) store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
+    for (int u = 0; u < APT; ++u) store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
   }
+  STAMP(2);
+  __syncthreads();  // plus counts complete
 
   // ---- phase 1b: iteration start + action select for owned agents --------
   // f64 value slots (-> slot t): 0 sumP, 1 sumP over C, 2 sumR, 3 sum w_P*P,
   // 4 sum w_rep*rr, 5 sum reward, 6 sum reward over C, 7 sum ratio over C
-  double va[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) va[k] = 0.0;
   uint32_t cw0 = 0, cw1 = 0;
-  uint64_t cwa = 0, cwb = 0;
   int own_bits[APT];  // a | so<<1 | s_t<<3
+  {
+    double va[8];
 #pragma unroll
-  for (int u = 0; u < APT; ++u) {
-    own_bits[u] = 0;
-    if (fin_only) continue;
-    const int r = rc[u] >> 16, c = rc[u] & 0xffff;
-    const uint32_t one = (vbits >> u) & 1;
-    const double vmu = one ? 1.0 : 0.0;
-    const int cs = (r + HS) * ly.sw + (c + HS);
-    const int ca = (r + HA) * ly.aw + (c + HA);
-    const int s_t = sS[cs] & 1;
-    const double P = payoff_rows(sM, r + HS, c + HS, tab, hp.norm_min, hp.norm_den, hp.norm_rcp);
-    const RVal<RQ> r_t = AS ? Rin[rb + gidx[u]] : sR[ca];
-    const double cmask = s_t ? 0.0 : vmu;
-    va[0] = __builtin_fma(P, vmu, va[0]);                 // spgg.py:388-390
-    va[1] = __builtin_fma(P, cmask, va[1]);
-    va[2] = __builtin_fma((double)r_t, vmu, va[2]);       // spgg.py:394 (units if RQ)
-    if (!acting) continue;
-    int so;                                               // spgg.py:409
-    if constexpr (AS) so = s_t == 0 ? 1 : 0;
-    else so = rep_state_lds<M2>(sR, ca, ly.aw);
-    int ex, rbt;                                          // algorithms.py:105-109
-    draw_pair<RNG>(a, rb, gidx[u], t, pkey, eps53, 0, &ex, &rbt);
-    double qs0, qs1;
-    select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
-    const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0
-    const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
-    const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
-    const double wpp = w_p * P, wrr = w_rep * rr;
-    const double rew = wpp + wrr;
-    sA[ca] = (uint8_t)act;
-    sRn[ca] = (RT)rn;
-    sRew[ca] = rew;
-    if (!(SPGG_ABLATE & 1024)) Rout[rb + gidx[u]] = (RT)rn;
-    own_bits[u] = act | (so << 1) | (s_t << 3);
-    cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
-    cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
-    cw1 += act == 0 ? one : 0u;
-    va[3] = __builtin_fma(wpp, vmu, va[3]);               // spgg.py:425-426
-    va[4] = __builtin_fma(wrr, vmu, va[4]);
-    va[5] = __builtin_fma(rew, vmu, va[5]);               // spgg.py:529-545
-    const double am = act ? 0.0 : vmu;
-    va[6] = __builtin_fma(rew, am, va[6]);
-    // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
-    if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
+    for (int k = 0; k < 8; ++k) va[k] = 0.0;
+#pragma unroll
+    for (int u = 0; u < APT; ++u) {
+      own_bits[u] = 0;
+      if (fin_only) continue;
+      const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+      const uint32_t one = (vbits >> u) & 1;
+      const double vmu = one ? 1.0 : 0.0;
+      const int cs = (r + HS) * ly.sw + (c + HS);
+      const int ca = (r + HA) * ly.aw + (c + HA);
+      const int s_t = sS[cs] & 1;
+      const double P = payoff_pc(sPC, r + HA, c + HA, tab + (s_t ? 6 : 0), hp.norm_min, hp.norm_den,
+                                 hp.norm_rcp);
+      const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sR[ca];
+      const double cmask = s_t ? 0.0 : vmu;
+      va[0] = __builtin_fma(P, vmu, va[0]);                 // spgg.py:388-390
+      va[1] = __builtin_fma(P, cmask, va[1]);
+      va[2] = __builtin_fma((double)r_t, vmu, va[2]);       // spgg.py:394 (units if RQ)
+      if (!acting) continue;
+      int so;                                               // spgg.py:409
+      if constexpr (AS) so = s_t == 0 ? 1 : 0;
+      else so = rep_state_lds<M2>(sR, ca, ly.aw);
+      int ex, rbt;                                          // algorithms.py:105-109
+      draw_pair<RNG>(a, rb, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
+      double qs0, qs1;
+      select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
+      const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0
+      const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
+      const double rr = act == 0 ? 0.5 : 0.0;               // spgg.py:424-427
+      const double wpp = w_p * P, wrr = w_rep * rr;
+      const double rew = wpp + wrr;
+      sA[ca] = (uint8_t)act;
+      sRn[ca] = (RT)rn;
+      sRew[ca] = rew;
+      *at(Rout, agent_of(rc[u])) = (RT)rn;
+      own_bits[u] = act | (so << 1) | (s_t << 3);
+      cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
+      cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
+      cw1 += act == 0 ? one : 0u;
+      va[3] = __builtin_fma(wpp, vmu, va[3]);               // spgg.py:425-426
+      va[4] = __builtin_fma(wrr, vmu, va[4]);
+      va[5] = __builtin_fma(rew, vmu, va[5]);               // spgg.py:529-545
+      const double am = act ? 0.0 : vmu;
+      va[6] = __builtin_fma(rew, am, va[6]);
+      // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
+      if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
+    }
+    // red[wave*64 + 16..23]: va[0..7] (reduced here: frees their registers for phases 1c / 2)
+    if (!(SPGG_ABLATE & 8)) wave_partials<8>(va, red, 16);
   }
+  STAMP(3);
 
   // ---- phase 1c: recompute the ring of neighbours (distance <= M) --------
   // Their Q row of state s_t (S_t bit 4) and max_diff come from the owner's
@@ -1017,8 +965,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
           }
         }
       }
-      const double P = payoff_rows(sM, ay + (HS - HA), ax + (HS - HA), tab, hp.norm_min, hp.norm_den,
-                                   hp.norm_rcp);
+      const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp);
       const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sR[ay * ly.aw + ax]);
       int ex, rbt;
       draw_pair<RNG>(a, rb, g, t, pkey, eps53, 0, &ex, &rbt);
@@ -1033,10 +980,11 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
     }
   }
   __syncthreads();
+  STAMP(4);
 
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;
-  [[maybe_unused]] double sink = 0.0;  // compute-only probe (SPGG_ABLATE & 1024)
+  uint32_t gcn = 0, nmd2 = 0;  // group composition nibbles GC0..5; NMD_POS2
   if (acting) {
     double* pout = a.pub_out + (size_t)(rep * a.tiles_per_rep + tile) * PF * a.PB;
 #pragma unroll
@@ -1049,14 +997,10 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      const float atd = td_update<ALG, RNG>(a, hp, rb, gidx[u], t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
+      const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
                                             act, sn, q[u], qb[u]);
-      if (SPGG_ABLATE & 1024) {
-        sink += q[u][0] + q[u][1] + q[u][2] + q[u][3] + (double)atd;
-      } else {
-        if (kappa != 0.0) a.atd[rb + gidx[u]] = atd;  // read only for the NI percent (0 when kappa == 0)
-        store_q<QB>(a.Q, rb + gidx[u], q[u], qb[u]);
-      }
+      if (kappa != 0.0) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
+      store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -1076,13 +1020,9 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = fmax(bmax, mdp);
-      if (SPGG_ABLATE & 1024) {
-        sink += mdp + (double)(own_bits[u] | (dp << 2) | (sn << 4));
-      } else {
-        a.md[rb + gidx[u]] = mdp;
-        a.S_out[rb + gidx[u]] = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
-      }
-      if (!(SPGG_ABLATE & 1024) && spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
+      *at(mdr, agent_of(rc[u])) = mdp;
+      *at(Sout, agent_of(rc[u])) = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
+      if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + spgg_impl::border_slot(r, c, th, tw, HA);
         rec[0] = sn ? q[u][2] : q[u][0];
         rec[a.PB] = sn ? q[u][3] : q[u][1];
@@ -1092,22 +1032,33 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         }
         rec[(PF - 1) * a.PB] = mdp;
       }
-      // group composition on S_{t+1}, spgg.py:585-592
+      // group composition on S_{t+1}, spgg.py:585-592: nibble nd of gcn
       const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
-      if (nd < 3) cwa += (uint64_t)one << (16 * (nd + 1));  // GC0..2: fields 5-7
-      else cwb += (uint64_t)one << (16 * (nd - 3));         // GC3..5: fields 8-10
+      gcn += one << (4 * nd);
       if (md > 0.0) {                                       // spgg.py:520-523
         cw1 += one << 16;
-        if (M2 && ks >= 4) cwa += one;
+        if (M2 && ks >= 4) nmd2 += one;
       }
     }
   }
-  if (!(SPGG_ABLATE & 8)) {  // red[wave*64 + 16..23]: va[0..7]; 24..29: counter words
-    wave_partials<8>(va, red, 16);
-    uint32_t cw[8] = {cw0, cw1, (uint32_t)cwa, (uint32_t)(cwa >> 32), (uint32_t)cwb, (uint32_t)(cwb >> 32), 0u, 0u};
+  STAMP(5);
+  if (!(SPGG_ABLATE & 8)) {  // red[wave*64 + 24..29]: counter words (fields of the layout above)
+    uint32_t cw[8] = {cw0,
+                      cw1,
+                      nmd2 | ((gcn & 0xfu) << 16),
+                      ((gcn >> 4) & 0xfu) | (((gcn >> 8) & 0xfu) << 16),
+                      ((gcn >> 12) & 0xfu) | (((gcn >> 16) & 0xfu) << 16),
+                      (gcn >> 20) & 0xfu,
+                      0u,
+                      0u};
     wave_partials<8>(cw, red, 24);
   }
+  {  // the tile's max(0, max_diff): wave maxima -> red[wave*64 + 12]
+    const double wm = wave_max(bmax);
+    if ((tid & 63) == 0) red[(tid >> 6) * 64 + 12] = wm;
+  }
   __syncthreads();
+  STAMP(6);
 
   // ---- workgroup totals -> per-iteration history record ------------------
   if ((SPGG_ABLATE & 8) && tid == 0 && tile == 0 && acting) srow[(size_t)(t + 1) * SPGG_NSTAT] = n / 2;
@@ -1138,6 +1089,15 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
       const bool start_val = (j <= 2 || j == 19);      // recorded on the absorbing iteration too
       if (k >= 0 && (acting || start_val)) slot = (j == 10) ? t + 1 : t;
     }
+    if (tid == 40 && acting) {  // lattice-wide max |diff| (spgg.py:488)
+      double bm = 0.0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) bm = fmax(bm, red[w * 64 + 12]);
+      // non-negative doubles order like their bit patterns
+      if (bm > 0.0)
+        atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
+                  (unsigned long long)__double_as_longlong(bm));
+    }
     if (slot >= 0) {
       const int j = tid - 16;
       const bool counter = j >= 8 && j <= 18;
@@ -1155,16 +1115,7 @@ __global__ __launch_bounds__(kBlock, SPGG_MIN_WAVES) void spgg_step_kernel(TileA
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);
     }
   }
-  if (SPGG_ABLATE & 1024) bmax += sink * 1e-300;  // keep the probe's results live
-  if (acting) {
-    __syncthreads();
-    const double bm = block_reduce_max(bmax, red);
-    if (tid == 0 && bm > 0.0) {
-      // non-negative doubles order like their bit patterns (spgg.py:488)
-      atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
-                (unsigned long long)__double_as_longlong(bm));
-    }
-  }
+  STAMP(7);
 }
 
 // Prologue of iteration 1: state s_1 of every agent into S_1 bit 4 and the
@@ -1279,6 +1230,13 @@ void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStrea
 #define SPGG_LAUNCH_EXTERN(k, name)                                                                 \
   extern template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t);
 #if SPGG_TU_HAS_ALG(0)
+#if SPGG_STAMPS
+}  // namespace spgg_impl
+extern "C" int spgg_stamps_read(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(spgg_stamps), bytes < sizeof(spgg_stamps) ? bytes : sizeof(spgg_stamps));
+}
+namespace spgg_impl {
+#endif
 SPGG_LAUNCH_INST(0, SPGG_ALG_QLEARNING)
 #else
 SPGG_LAUNCH_EXTERN(0, SPGG_ALG_QLEARNING)
@@ -1607,6 +1565,8 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   if (cfg->algorithm < SPGG_ALG_QLEARNING || cfg->algorithm > SPGG_ALG_DOUBLE_Q) return SPGG_E_ARG;
   if (cfg->iterations >= (1 << 26)) return SPGG_E_ARG;  // Philox counter: t + pair*2^26
   if ((long long)cfg->n_rep * cfg->L * cfg->L > (1LL << 31) - 1) return SPGG_E_ARG;
+  // the step kernel addresses a replica's arrays with 32-bit byte offsets (Q: qw doubles per agent)
+  if ((long long)cfg->L * cfg->L * spgg_impl::qw_of(cfg->algorithm) * 8 > 0xFFFFFFFFLL) return SPGG_E_ARG;
   spgg_ctx* c = new (std::nothrow) spgg_ctx();
   if (!c) return SPGG_E_ARG;
   c->cfg = *cfg;

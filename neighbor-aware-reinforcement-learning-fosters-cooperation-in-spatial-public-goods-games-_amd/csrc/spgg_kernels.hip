@@ -167,10 +167,14 @@ constexpr int kPcPitch = 64;
 // 16-byte aligned carve: f64 first, then the R planes (rsz = 8 or 1), then bytes.
 // S and defector-bit planes: tile + halo HS (payoffs over tile + HA); the
 // plus-count plane: tile + HA + 1 rows of kPcPitch; everything else tile + HA.
-__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, int rsz) {
+// dword_rows (compile-time-width kernels): every plane has one dword-aligned
+// pitch wide enough for a window staged as aligned dwords (window column j at
+// plane column j + its 0..3-byte misalignment).
+__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, int rsz, bool dword_rows = false) {
   LdsLayout l;
   l.sw = tw + 2 * HS; l.sh = th + 2 * HS;
   l.aw = tw + 2 * HA; l.ah = th + 2 * HA;
+  if (dword_rows) l.sw = l.aw = (tw + 2 * HS + 3 + 3) / 4 * 4;
   const int na = l.aw * l.ah;
   int off = (12 + kWaves * 64) * 8;  // payoff table + reduction scratch
   l.off_Rew = off;  off += ((na * 8 + 15) / 16) * 16;
@@ -374,6 +378,45 @@ struct RowWindow {
   }
 };
 
+// Window of h rows staged as aligned dwords (TWC kernels, L % 4 == 0, tile
+// columns multiples of 4): xb = the window's first global column rounded down
+// to a multiple of 4 (may be negative: periodic), DW dwords per row, flattened
+// over the workgroup (J >= h*DW / kBlock, host-checked via TH <= 25).  A
+// 46-byte row costs 12-13 lanes instead of 46 byte loads, one VGPR per J.
+template <int J, int DW>
+struct DwordWindow {
+  uint32_t buf[J];
+  __device__ __forceinline__ void load(const void* plane, int h, int y0, int xb, int L) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(plane);
+    const int tid = threadIdx.x, Ld = L >> 2, xd0 = xb >> 2;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {  // unconditional loads (rows clamped)
+      const int k = tid + j * kBlock;
+      const int row = min(k / DW, h - 1), col = k - (k / DW) * DW;
+      int gy = y0 + row;
+      gy += gy < 0 ? L : 0;
+      gy -= gy >= L ? L : 0;
+      int gx = xd0 + col;
+      gx += gx < 0 ? Ld : 0;
+      gx -= gx >= Ld ? Ld : 0;
+      buf[j] = *at(src, (uint32_t)(gy * Ld + gx));
+    }
+  }
+  // dst (pitch bytes, a multiple of 4): the window's dwords; dbit: bit0 of each byte.
+  __device__ __forceinline__ void store(uint8_t* dst, int pitch, int h, uint8_t* dbit) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int k = tid + j * kBlock;
+      if (k < h * DW) {
+        const int o = (k / DW) * pitch + (k - (k / DW) * DW) * 4;
+        *reinterpret_cast<uint32_t*>(dst + o) = buf[j];
+        if (dbit) *reinterpret_cast<uint32_t*>(dbit + o) = buf[j] & 0x01010101u;
+      }
+    }
+  }
+};
+
 // Plus-shaped defector counts over the region + 1 ring, x8 (byte offsets into
 // a payoff table indexed by defector count): pc[(y)*64 + x] for region cell
 // (y - 1, x - 1) = defector bits of S-window cells (y+1, x+1) and its four
@@ -415,6 +458,13 @@ __device__ __forceinline__ double rcp_diag(double x) {
   r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
   r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
   return r;
+}
+
+// Eight signed bytes packed little-endian into a 64-bit immediate.
+constexpr uint64_t stat_bytes(int a, int b, int c, int d, int e, int f, int g, int h) {
+  return (uint64_t)(uint8_t)a | (uint64_t)(uint8_t)b << 8 | (uint64_t)(uint8_t)c << 16 | (uint64_t)(uint8_t)d << 24 |
+         (uint64_t)(uint8_t)e << 32 | (uint64_t)(uint8_t)f << 40 | (uint64_t)(uint8_t)g << 48 |
+         (uint64_t)(uint8_t)h << 56;
 }
 
 // History counters as 16-bit fields f = 0..10, two per dword (word f>>1,
@@ -662,7 +712,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const int th = min(a.TH, L - y0), tw = TWC ? TWC : min(a.TW, L - x0);
   // LDS pitches from the full tile width (constants when TWC > 0); edge tiles
   // use the top-left part of each region
-  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HA, (int)sizeof(RT))
+  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HA, (int)sizeof(RT), true)
                            : lds_layout(tw, th, HS, HA, (int)sizeof(RT));
   double* tab = reinterpret_cast<double*>(smem);
   double* red = tab + 12;
@@ -747,14 +797,26 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
     for (int j = 0; j < RP; ++j) re[j] = *at(rtab, (uint32_t)min(tid + j * kBlock, ring - 1));
   }
-  // halo windows into registers (TWC: row-per-wave; rows <= TH + 2*halo, TH <= 25 host-checked)
-  constexpr int JSR = (25 + 2 * HS + kWaves - 1) / kWaves, JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
+  // halo windows into registers (TWC: aligned dwords, or rows of f64 R per
+  // wave; rows <= TH + 2*halo, TH <= 25 host-checked)
+  constexpr int JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
   constexpr int JSF = spgg_impl::js_of(M2), JRF = spgg_impl::jr_of();
-  RowWindow<JSR, TWC + 2 * HS, uint8_t> winS;
+  constexpr int DWS = (TWC + 2 * HS + 3 + 3) / 4, DWR = (TWC + 2 * HA + 3 + 3) / 4;
+  constexpr int JSD = ((25 + 2 * HS) * DWS + kBlock - 1) / kBlock, JRD = ((25 + 2 * HA) * DWR + kBlock - 1) / kBlock;
+  // window column j lives at plane column j + its misalignment (views below)
+  const int soffS = TWC ? ((x0 - HS) & 3) : 0, soffR = TWC && RQ ? ((x0 - HA) & 3) : 0;
+  uint8_t* sSv = sS + soffS;  // S / defector planes indexed by window coordinates
+  uint8_t* sDv = sD + soffS;
+  RT* sRv = sR + soffR;
+  DwordWindow<JSD, DWS> winS;
+  DwordWindow<JRD, DWR> winRd;
   RowWindow<JRR, TWC + 2 * HA, RT> winR;
   if constexpr (TWC > 0) {
-    winS.load(Sin, th + 2 * HS, y0 - HS, x0 - HS, L);
-    if (!AS) winR.load(Rin, ah, y0 - HA, x0 - HA, L);
+    winS.load(Sin, th + 2 * HS, y0 - HS, (x0 - HS) & ~3, L);
+    if constexpr (!AS) {
+      if constexpr (RQ) winRd.load(Rin, ah, y0 - HA, (x0 - HA) & ~3, L);
+      else winR.load(Rin, ah, y0 - HA, x0 - HA, L);
+    }
   }
 
   // replica state (scalar loads)
@@ -789,8 +851,11 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 
   // windows -> LDS (waits for the loads above)
   if constexpr (TWC > 0) {
-    winS.template store<TWC + 2 * HS>(sS, th + 2 * HS, sD);
-    if (!AS) winR.template store<TWC + 2 * HA>(sR, ah, nullptr);
+    winS.store(sS, ly.sw, th + 2 * HS, sD);
+    if constexpr (!AS) {
+      if constexpr (RQ) winRd.store(reinterpret_cast<uint8_t*>(sR), ly.aw, ah, nullptr);
+      else winR.template store<(TWC + 2 * HS + 6) / 4 * 4>(sR, ah, nullptr);
+    }
   } else {
     stage_region<JSF>(sS, ly.sw, Sin, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny, sD);
     if (!AS) stage_region<JRF>(sR, ly.aw, Rin, ah, aw, y0 - HA, x0 - HA, L, tiny);
@@ -817,13 +882,13 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
       *at(mdr, agent_of(rc[u])) = md_own[u];
       *at(atdr, agent_of(rc[u])) = atd_own[u];
-      *at(Sout, agent_of(rc[u])) = sS[(r + HS) * ly.sw + (c + HS)];
-      if (!AS) *at(Rout, agent_of(rc[u])) = sR[(r + HA) * ly.aw + (c + HA)];
+      *at(Sout, agent_of(rc[u])) = sSv[(r + HS) * ly.sw + (c + HS)];
+      if (!AS) *at(Rout, agent_of(rc[u])) = sRv[(r + HA) * ly.aw + (c + HA)];
     }
     return;
   }
   // plus counts for the payoffs of phases 1b / 1c (their barrier: after phase 1a)
-  if (!fin_only) build_plus_counts(sPC, sD, ly.sw, ah + 2);
+  if (!fin_only) build_plus_counts(sPC, sDv, ly.sw, ah + 2);
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
   // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C, 8 NI percent
@@ -837,7 +902,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       for (int u = 0; u < APT; ++u) {
         const double vmu = (vbits >> u) & 1 ? 1.0 : 0.0;
         const int r = rc[u] >> 16, c = rc[u] & 0xffff;
-        const uint8_t b = sS[(r + HS) * ly.sw + (c + HS)];
+        const uint8_t b = sSv[(r + HS) * ly.sw + (c + HS)];
         const int e = pending_entry(b);
         // kappa == 0 (a replica-uniform skip): nu = +0, q + 0 == q (Q never holds -0.0:
         // U(-0.01,0.01) draws and TD sums of finite values give +0 for exact zeros),
@@ -894,10 +959,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const double vmu = one ? 1.0 : 0.0;
       const int cs = (r + HS) * ly.sw + (c + HS);
       const int ca = (r + HA) * ly.aw + (c + HA);
-      const int s_t = sS[cs] & 1;
+      const int s_t = sSv[cs] & 1;
       const double P = payoff_pc(sPC, r + HA, c + HA, tab + (s_t ? 6 : 0), hp.norm_min, hp.norm_den,
                                  hp.norm_rcp);
-      const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sR[ca];
+      const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sRv[ca];
       const double cmask = s_t ? 0.0 : vmu;
       va[0] = __builtin_fma(P, vmu, va[0]);                 // spgg.py:388-390
       va[1] = __builtin_fma(P, cmask, va[1]);
@@ -905,7 +970,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       if (!acting) continue;
       int so;                                               // spgg.py:409
       if constexpr (AS) so = s_t == 0 ? 1 : 0;
-      else so = rep_state_lds<M2>(sR, ca, ly.aw);
+      else so = rep_state_lds<M2>(sRv, ca, ly.aw);
       int ex, rbt;                                          // algorithms.py:105-109
       draw_pair<RNG>(a, rb, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
       double qs0, qs1;
@@ -949,7 +1014,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       spgg_impl::ring_cell(k, th, tw, HA, &ay, &ax);
       const int g = re[j].x;
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
-      const uint8_t b = sS[cs];
+      const uint8_t b = sSv[cs];
       double v0 = rv[j][0], v1 = rv[j][1], w0 = 0.0, w1 = 0.0;
       if constexpr (QB) {
         w0 = rv[j][QB ? 2 : 0];
@@ -966,7 +1031,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         }
       }
       const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp);
-      const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sR[ay * ly.aw + ax]);
+      const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sRv[ay * ly.aw + ax]);
       int ex, rbt;
       draw_pair<RNG>(a, rb, g, t, pkey, eps53, 0, &ex, &rbt);
       const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
@@ -1076,13 +1141,17 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
     } else if (tid >= 16 && tid < 16 + 22 && !fin_only) {
       const int j = tid - 16;  // 0-7 va, 8-18 counters, 19-20 derived
-      static constexpr int kmap[22] = {
-          SPGG_ST_SUMP, SPGG_ST_SUMP_C, SPGG_ST_SUMR, SPGG_ST_SUM_WPP, SPGG_ST_SUM_WRR,
-          -1 /* reward total: only feeds REW_D */, SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C,
-          SPGG_ST_SW_CD, SPGG_ST_SW_DC, SPGG_ST_NCOOP, SPGG_ST_NMD_POS, SPGG_ST_NMD_POS2,
-          SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2, SPGG_ST_GC0 + 3, SPGG_ST_GC0 + 4,
-          SPGG_ST_GC0 + 5, SPGG_ST_SUMP_D, SPGG_ST_SUM_REW_D, -1};
-      k = kmap[j];
+      // record index of value j, one byte each in three 64-bit immediates (a
+      // constant-memory table would cost the epilogue a memory round trip)
+      constexpr uint64_t km0 = stat_bytes(SPGG_ST_SUMP, SPGG_ST_SUMP_C, SPGG_ST_SUMR, SPGG_ST_SUM_WPP,
+                                          SPGG_ST_SUM_WRR, -1 /* reward total: only feeds REW_D */,
+                                          SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C);
+      constexpr uint64_t km1 = stat_bytes(SPGG_ST_SW_CD, SPGG_ST_SW_DC, SPGG_ST_NCOOP, SPGG_ST_NMD_POS,
+                                          SPGG_ST_NMD_POS2, SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2);
+      constexpr uint64_t km2 = stat_bytes(SPGG_ST_GC0 + 3, SPGG_ST_GC0 + 4, SPGG_ST_GC0 + 5, SPGG_ST_SUMP_D,
+                                          SPGG_ST_SUM_REW_D, -1, -1, -1);
+      const uint64_t km = j < 8 ? km0 : (j < 16 ? km1 : km2);
+      k = (int)(int8_t)(uint8_t)(km >> (8 * (j & 7)));
       src = 16 + j;
       if (j == 19) { src = 16 + 0; src_c = 16 + 1; }   // sumP over D = sumP - sumP over C
       if (j == 20) { src = 16 + 5; src_c = 16 + 6; }   // reward over D = total - over C
@@ -1406,6 +1475,13 @@ struct spgg_ctx {
 
 namespace {
 
+// Compile-time tile width of the step kernel (0: run-time width): every tile
+// full width, L >= 2 * window width (L % 4 == 0 for the aligned-dword window
+// staging), window rows within the staging register budget (TH <= 25).
+int twc_of(const spgg_config& cfg, int TW, int TH) {
+  return (TW == 40 && cfg.L % 40 == 0 && cfg.L >= 120 && TH <= 25) ? 40 : 0;
+}
+
 int fail(spgg_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
@@ -1523,9 +1599,7 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   lc.as = c->cfg.state_mode == SPGG_STATE_ACTION;
   lc.rq = c->cfg.rep_int8 != 0;
   lc.rng = c->cfg.rng_mode;
-  // compile-time-width kernels: every tile full width, L >= 2 * window width,
-  // window rows within the row-per-wave register budget (4 * JSR / JRR)
-  lc.twc = (c->TW == 40 && c->cfg.L % 40 == 0 && c->cfg.L >= 120 && c->TH <= 25) ? 40 : 0;
+  lc.twc = twc_of(c->cfg, c->TW, c->TH);
   lc.total_tiles = c->cfg.n_rep * c->tiles_per_rep;
   lc.lds_bytes = c->lds_bytes;
   switch (c->cfg.algorithm) {
@@ -1584,7 +1658,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->tiles_x = (cfg->L + c->TW - 1) / c->TW;
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
   const int HA = cfg->second_order ? 2 : 1;
-  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8);
+  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8, twc_of(*cfg, c->TW, c->TH) > 0);
   c->lds_bytes = (size_t)ly.bytes;
   c->PB = spgg_impl::pub_slots(c->TW, c->TH, HA);
   // stage_region's per-thread register window must cover the S and R halos

@@ -62,41 +62,55 @@ def workload(name, rank):
 def cpu_baseline(L, M2, state, reps, budget_s=15.0):
     """Oracle (NumPy restatement of the reference step, same diagnostics) on host cores.
 
-    Bounded sample: up to 16 replicas of the same workload, each run by its own
-    process (the reference's own Pool parallelism, runner.py:142) for as many
-    iterations as fit the budget."""
+    Bounded sample of the same workload: up to 16 replicas, each stepped by its
+    own process (the reference's own Pool parallelism, runner.py:142) for
+    budget_s of wall time after a short warm-up; the rate counts the agent-steps
+    those processes completed inside their timed windows."""
     import multiprocessing as mp
-    import numpy as np
-    from oracle import spgg_oracle as O
     procs = max(1, min(16, os.cpu_count() or 1, len(reps)))
-    # calibrate one step on this host
-    t0 = time.perf_counter()
-    _cpu_job((L, M2, state, reps[0], 3))
-    per_step = (time.perf_counter() - t0) / 3
-    iters = max(5, int(budget_s / max(per_step, 1e-6)))
-    jobs = [(L, M2, state, reps[i % len(reps)], iters) for i in range(procs)]
-    t0 = time.perf_counter()
+    jobs = [(L, M2, state, reps[i % len(reps)], budget_s) for i in range(procs)]
     with mp.get_context("fork").Pool(procs) as pool:
         done = pool.map(_cpu_job, jobs)
-    wall = time.perf_counter() - t0
-    agent_steps = sum(done) * L * L
+    steps = sum(d[0] for d in done)
+    wall = max(d[1] for d in done)
+    agent_steps = steps * L * L
     return {"value": agent_steps / wall, "unit": "agent-steps/s", "cores": procs, "kind": "port",
-            "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics), {procs} processes x "
-                      f"{iters} iterations of L={L} replicas from the same workload; "
-                      f"{sum(done)} iterations in {wall:.1f}s wall"}
+            "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics), {procs} processes, each stepping "
+                      f"one L={L} replica of the same workload for {budget_s:.0f} s after 3 warm-up "
+                      f"iterations; {steps} iterations in {wall:.1f} s wall"}
+
+
+class _Budget(Exception):
+    pass
 
 
 def _cpu_job(job):
+    """Step one replica with the oracle until the time budget is spent: (iterations, seconds)."""
     import numpy as np
     from oracle import spgg_oracle as O
-    L, M2, state, p, iters = job
-    op = O.Params(L=L, iterations=iters, use_second_order=M2, state_representation=state,
+    L, M2, state, p, budget = job
+    op = O.Params(L=L, iterations=10 ** 9, use_second_order=M2, state_representation=state,
                   **{k: getattr(p, k) for k in ("r", "c", "cost", "alpha", "gamma", "epsilon",
                                                  "epsilon_decay", "epsilon_min", "influence_factor",
                                                  "lambda_epsilon", "delta_R_D", "R_min", "R_max",
                                                  "reward_weight_payoff", "rep_gain_C")})
-    _, fin = O.run(op, np.random.RandomState(p.seed or 0), collect_snapshots=False)
-    return fin["stop_iter"] - 1 if fin["stop_iter"] else iters
+    clock = {"t0": None, "n": 0}
+
+    def on_step(i, *_):
+        if i == 3:                       # warm-up done: start the timed window
+            clock["t0"] = time.perf_counter()
+        elif i > 3:
+            clock["n"] += 1
+            if time.perf_counter() - clock["t0"] >= budget:
+                raise _Budget()
+
+    try:
+        O.run(op, np.random.RandomState(p.seed or 0), collect_snapshots=False, on_step=on_step)
+    except _Budget:
+        pass
+    if clock["t0"] is None:              # absorbed during warm-up (not the bench workload)
+        return 0, 1e-9
+    return clock["n"], time.perf_counter() - clock["t0"]
 
 
 def main():

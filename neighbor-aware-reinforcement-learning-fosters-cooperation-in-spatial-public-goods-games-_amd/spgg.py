@@ -66,7 +66,7 @@ class SPGG:
         self._Sn = S_in_one
         self.create_population()
 
-        self.track_positions = [(L // 2, L // 2), (L // 4, L // 4), (3 * L // 4, 3 * L // 4)]
+        self.track_positions = track_positions(L)
         self.q_history = {pos: {'q_c': [], 'q_d': []} for pos in self.track_positions}
         self.it_records = []
         self.epsilon_history = []
@@ -147,40 +147,7 @@ class SPGG:
         finally:
             eng.close()
 
-        with open_writer(filename) as data_file:
-            for i in sorted(snaps):
-                Ri, Si = snaps[i]
-                data_file.create_dataset(f"R_snapshot_{i}", data=Ri)
-                h, bins = np.histogram(Ri, bins=20, range=(self.R_min, self.R_max))
-                data_file.create_dataset(f"rep_hist_{i}", data=h)
-                data_file.create_dataset(f"rep_bins_{i}", data=bins)
-                data_file.create_dataset(f"Sn_snapshot_{i}", data=Si)
-            for name in ("it_records_final", "epsilon_history_final", "rep_avg_history_final",
-                         "coop_rate_history", "switch_C_to_D", "switch_D_to_C",
-                         "neighbor_influence_percent", "payoff_component_history",
-                         "rep_component_history", "best_neighbor_second_order_percent",
-                         "reputation_reward_ratio", "avg_reward_C_history", "avg_reward_D_history"):
-                data_file.create_dataset(name, data=hist[name])
-            for d in range(6):
-                data_file.create_dataset(f"group_comp_d{d}_history", data=hist[f"group_comp_d{d}_history"])
-            for grp in ("cooperators", "defectors"):
-                for s in ("s0", "s1"):
-                    for a in ("c", "d"):
-                        k = f"{grp}_q_{s}_{a}_history"
-                        data_file.create_dataset(k, data=hist[k])
-            for s in ("s0", "s1"):
-                for a in ("c", "d"):
-                    k = f"avg_q_{s}_{a}_history"
-                    data_file.create_dataset(k, data=hist[k])
-            for p_ in self.track_positions:  # never filled by the reference (spgg.py:345,620-622)
-                data_file.create_dataset(f"q_c_pos_{p_[0]}_{p_[1]}_final", data=np.array([]))
-                data_file.create_dataset(f"q_d_pos_{p_[0]}_{p_[1]}_final", data=np.array([]))
-            data_file.create_dataset("Sn_final", data=S)
-            data_file.create_dataset("R_final", data=R)
-            h, bins = np.histogram(R, bins=20, range=(self.R_min, self.R_max))
-            data_file.create_dataset("rep_hist_final", data=h)
-            data_file.create_dataset("rep_bins_final", data=bins)
-            data_file.create_dataset("cluster_sizes", data=cluster_sizes(S))
+        write_datasets(filename, hist, snaps, S, R, self.R_min, self.R_max, self.track_positions)
 
         if self.save_png and frames:
             _write_pngs(frames, snapshots_dir)
@@ -201,6 +168,55 @@ class SPGG:
         S_coop = (S == 0).astype(int)
         S_def = (S == 1).astype(int)
         return (np.sum(S_coop) / (L * L), np.sum(S_def) / (L * L), np.mean(P))
+
+
+
+HISTORY_DATASETS = ("it_records_final", "epsilon_history_final", "rep_avg_history_final",
+                    "coop_rate_history", "switch_C_to_D", "switch_D_to_C",
+                    "neighbor_influence_percent", "payoff_component_history",
+                    "rep_component_history", "best_neighbor_second_order_percent",
+                    "reputation_reward_ratio", "avg_reward_C_history", "avg_reward_D_history")
+
+
+def write_datasets(filename, hist, snaps, S, R, R_min, R_max, track_positions):
+    """The dataset layout `SPGG.run` writes (spgg.py:594-633): snapshots, the
+    per-iteration histories, the never-filled tracked-position Q datasets and
+    the final state.  Shared by SPGG.run and the batched sweep runner."""
+    with open_writer(filename) as data_file:
+        for i in sorted(snaps):
+            Ri, Si = snaps[i]
+            data_file.create_dataset(f"R_snapshot_{i}", data=Ri)
+            h, bins = np.histogram(Ri, bins=20, range=(R_min, R_max))
+            data_file.create_dataset(f"rep_hist_{i}", data=h)
+            data_file.create_dataset(f"rep_bins_{i}", data=bins)
+            data_file.create_dataset(f"Sn_snapshot_{i}", data=Si)
+        for name in HISTORY_DATASETS:
+            data_file.create_dataset(name, data=hist[name])
+        for d in range(6):
+            data_file.create_dataset(f"group_comp_d{d}_history", data=hist[f"group_comp_d{d}_history"])
+        for grp in ("cooperators", "defectors"):
+            for s in ("s0", "s1"):
+                for a in ("c", "d"):
+                    k = f"{grp}_q_{s}_{a}_history"
+                    data_file.create_dataset(k, data=hist[k])
+        for s in ("s0", "s1"):
+            for a in ("c", "d"):
+                k = f"avg_q_{s}_{a}_history"
+                data_file.create_dataset(k, data=hist[k])
+        for p_ in track_positions:  # never filled by the reference (spgg.py:345,620-622)
+            data_file.create_dataset(f"q_c_pos_{p_[0]}_{p_[1]}_final", data=np.array([]))
+            data_file.create_dataset(f"q_d_pos_{p_[0]}_{p_[1]}_final", data=np.array([]))
+        data_file.create_dataset("Sn_final", data=S)
+        data_file.create_dataset("R_final", data=R)
+        h, bins = np.histogram(R, bins=20, range=(R_min, R_max))
+        data_file.create_dataset("rep_hist_final", data=h)
+        data_file.create_dataset("rep_bins_final", data=bins)
+        data_file.create_dataset("cluster_sizes", data=cluster_sizes(S))
+
+
+def track_positions(L):
+    """Positions whose Q the reference meant to track (spgg.py:143)."""
+    return [(L // 2, L // 2), (L // 4, L // 4), (3 * L // 4, 3 * L // 4)]
 
 
 def cluster_sizes(S):

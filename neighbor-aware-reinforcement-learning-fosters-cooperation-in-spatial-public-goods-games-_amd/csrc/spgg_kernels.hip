@@ -213,13 +213,14 @@ using RVal = typename std::conditional<RQ, int, double>::type;
 // agents' stores may alias them and reloads them per agent).
 struct HotParams {
   double norm_min, norm_den, norm_rcp, alpha, gamma, diag_alpha, diag_gamma;
-  double rep_gain_c, neg_delta_r_d, r_min, r_max;
+  double rep_gain_c, neg_delta_r_d, r_min, r_max, rep_unit;
   int rk_gain, rk_loss, rk_min, rk_max;
 };
 
 __device__ __forceinline__ HotParams hot_params(const spgg_rep_params& p) {
   return HotParams{p.norm_min, p.norm_den, p.norm_rcp, p.alpha, p.gamma, p.diag_alpha, p.diag_gamma,
-                   p.rep_gain_c, p.neg_delta_r_d, p.r_min, p.r_max, p.rk_gain, p.rk_loss, p.rk_min, p.rk_max};
+                   p.rep_gain_c, p.neg_delta_r_d, p.r_min, p.r_max, p.rep_unit, p.rk_gain, p.rk_loss, p.rk_min,
+                   p.rk_max};
 }
 
 template <bool RQ, typename PT>
@@ -982,8 +983,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const double rew = wpp + wrr;
       sA[ca] = (uint8_t)act;
       sRn[ca] = (RT)rn;
-      sRew[ca] = rew;
-      *at(Rout, agent_of(rc[u])) = (RT)rn;
+      sRew[ca] = rew;  // (R_{t+1} is stored in phase 2: a store here would make the ring's
+                       // record loads wait for it)
       own_bits[u] = act | (so << 1) | (s_t << 3);
       cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
       cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
@@ -1087,6 +1088,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       bmax = fmax(bmax, mdp);
       *at(mdr, agent_of(rc[u])) = mdp;
       *at(Sout, agent_of(rc[u])) = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
+      *at(Rout, agent_of(rc[u])) = sRn[ca];
       if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + spgg_impl::border_slot(r, c, th, tw, HA);
         rec[0] = sn ? q[u][2] : q[u][0];
@@ -1178,7 +1180,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
       double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
       if (counter) val = (double)(((unsigned long long)tot[0] >> (16 * ((j - 8) & 1))) & 0xffffu);
-      if (RQ && k == SPGG_ST_SUMR) val *= pg.rep_unit;
+      // (from LDS: a global read here would wait for every store of the tile)
+      if (RQ && k == SPGG_ST_SUMR) val *= hp.rep_unit;
       if (k == SPGG_ST_SUM_PCT || k == SPGG_ST_SUM_RATIO_C) val *= 100.0;  // percent sums
       if (val != 0.0 && (!(SPGG_ABLATE & 2) || k == SPGG_ST_NCOOP))
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);

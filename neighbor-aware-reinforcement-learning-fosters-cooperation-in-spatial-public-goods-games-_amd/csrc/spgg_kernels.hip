@@ -756,7 +756,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   // tile's first agent (same inputs, so every value it computes and stores is
   // bit-identical to the owner's); only its history contributions are masked
   // (vm = 0).  Per-slot branches cost more in exec-mask and copy instructions.
-  int rc[APT];  // (r << 16) | c of slot u; its agent index is agent_of(rc[u]) (recomputed, not held)
+  // slot u: (r << 16) | (c << 8) | its action bits (a | s_old << 1 | dp << 2 | s_t << 3 | s' << 4, set
+  // from phase 1b on); the agent index is agent_of(rc[u]) (recomputed, not held)
+  int rc[APT];
   unsigned vbits = 0;  // bit u: slot u holds an owned agent
   double q[APT][4];
   double qb[APT][QB ? 4 : 1];
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   float atd_own[APT];
   const int n_own = th * tw;
   const uint32_t g00 = (uint32_t)(y0 * L + x0);
-  auto agent_of = [&](int rcu) { return g00 + (uint32_t)((rcu >> 16) * L + (rcu & 0xffff)); };
+  auto agent_of = [&](int rcu) { return g00 + (uint32_t)((rcu >> 16) * L + ((rcu >> 8) & 0xff)); };
   {
     const int dr = kBlock / tw, dc = kBlock - (kBlock / tw) * tw;
     int r = tid / tw, c = tid - (tid / tw) * tw;
@@ -772,7 +774,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     for (int u = 0; u < APT; ++u) {
       const int k = tid + u * kBlock;
       const bool own = k < n_own;
-      rc[u] = own ? (r << 16) | c : 0;
+      rc[u] = own ? (r << 16) | (c << 8) : 0;
       vbits |= own ? 1u << u : 0u;
       // loads unconditional (threads without a u-th agent read the tile's
       // first one and drop it; md/atd are read even at t = 1, unused there):
@@ -879,7 +881,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (SPGG_ABLATE & 128) {  // memory floor: write back what was read
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
-      const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+      const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
       store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
       *at(mdr, agent_of(rc[u])) = md_own[u];
       *at(atdr, agent_of(rc[u])) = atd_own[u];
@@ -902,7 +904,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
         const double vmu = (vbits >> u) & 1 ? 1.0 : 0.0;
-        const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+        const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
         const uint8_t b = sSv[(r + HS) * ly.sw + (c + HS)];
         const int e = pending_entry(b);
         // kappa == 0 (a replica-uniform skip): nu = +0, q + 0 == q (Q never holds -0.0:
@@ -939,23 +941,36 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
     for (int u = 0; u < APT; ++u) store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
   }
+  // the ring cells' border records (landed during phase 1a) to LDS for phase 1c:
+  // held in registers across phase 1b they cost the occupancy of a fifth wave
+  double* sRec = reinterpret_cast<double*>(smem + ly.bytes);  // [ring cell][PF]
+#pragma unroll
+  for (int j = 0; j < RP; ++j) {
+    const int k = tid + j * kBlock;
+    if (k < ring) {
+#pragma unroll
+      for (int f = 0; f < PF; ++f) sRec[k * PF + f] = rv[j][f];
+    }
+  }
   STAMP(2);
-  __syncthreads();  // plus counts complete
+  __syncthreads();  // plus counts and ring records complete
 
   // ---- phase 1b: iteration start + action select for owned agents --------
   // f64 value slots (-> slot t): 0 sumP, 1 sumP over C, 2 sumR, 3 sum w_P*P,
-  // 4 sum w_rep*rr, 5 sum reward, 6 sum reward over C, 7 sum ratio over C
+  // 4 sum w_rep*rr, 5 sum reward, 6 sum reward over C, 7 sum ratio over C.
+  // Slots 4 and 5 are not accumulated: w_rep*rr is w_rep*0.5 for every
+  // cooperating action and 0 otherwise, so slot 4 = (C actions) * w_rep*0.5 and
+  // slot 5 = slot 3 + slot 4 (history means, tolerance 1e-5; slot 5 only feeds
+  // the defectors' reward mean as total - over C).
   uint32_t cw0 = 0, cw1 = 0;
-  int own_bits[APT];  // a | so<<1 | s_t<<3
   {
     double va[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) va[k] = 0.0;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
-      own_bits[u] = 0;
       if (fin_only) continue;
-      const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+      const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
       const uint32_t one = (vbits >> u) & 1;
       const double vmu = one ? 1.0 : 0.0;
       const int cs = (r + HS) * ly.sw + (c + HS);
@@ -985,18 +1000,18 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       sRn[ca] = (RT)rn;
       sRew[ca] = rew;  // (R_{t+1} is stored in phase 2: a store here would make the ring's
                        // record loads wait for it)
-      own_bits[u] = act | (so << 1) | (s_t << 3);
+      rc[u] |= act | (so << 1) | (s_t << 3);
       cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
       cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
       cw1 += act == 0 ? one : 0u;
       va[3] = __builtin_fma(wpp, vmu, va[3]);               // spgg.py:425-426
-      va[4] = __builtin_fma(wrr, vmu, va[4]);
-      va[5] = __builtin_fma(rew, vmu, va[5]);               // spgg.py:529-545
       const double am = act ? 0.0 : vmu;
       va[6] = __builtin_fma(rew, am, va[6]);
       // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
       if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
     }
+    va[4] = (double)(cw1 & 0xffffu) * (w_rep * 0.5);      // spgg.py:425-426
+    va[5] = va[3] + va[4];                                  // spgg.py:529-545
     // red[wave*64 + 16..23]: va[0..7] (reduced here: frees their registers for phases 1c / 2)
     if (!(SPGG_ABLATE & 8)) wave_partials<8>(va, red, 16);
   }
@@ -1016,15 +1031,16 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int g = re[j].x;
       const int cs = (ay + (HS - HA)) * ly.sw + (ax + (HS - HA));
       const uint8_t b = sSv[cs];
-      double v0 = rv[j][0], v1 = rv[j][1], w0 = 0.0, w1 = 0.0;
+      const double* rec = sRec + k * PF;
+      double v0 = rec[0], v1 = rec[1], w0 = 0.0, w1 = 0.0;
       if constexpr (QB) {
-        w0 = rv[j][QB ? 2 : 0];
-        w1 = rv[j][QB ? 3 : 0];
+        w0 = rec[QB ? 2 : 0];
+        w1 = rec[QB ? 3 : 0];
       }
       if (pending && kappa != 0.0) {  // kappa == 0: nu = +0 (see phase 1a)
         const int e = pending_entry(b);
         if ((e >> 1) == ((b >> 4) & 1)) {  // the NI entry lies in the published row
-          const double nu = pending_nu(b, rv[j][PF - 1], kappa, lam_den, lam_rcp);
+          const double nu = pending_nu(b, rec[PF - 1], kappa, lam_den, lam_rcp);
           if (e & 1) v1 = v1 + nu; else v0 = v0 + nu;
           if constexpr (QB) {
             if (e & 1) w1 = w1 + nu; else w0 = w0 + nu;
@@ -1055,10 +1071,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     double* pout = a.pub_out + (size_t)(rep * a.tiles_per_rep + tile) * PF * a.PB;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
-      const int r = rc[u] >> 16, c = rc[u] & 0xffff;
+      const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
       const int ca = (r + HA) * ly.aw + (c + HA);
       const uint32_t one = (vbits >> u) & 1;
-      const int act = own_bits[u] & 1, so = (own_bits[u] >> 1) & 1;
+      const int act = rc[u] & 1, so = (rc[u] >> 1) & 1;
       const double rew = sRew[ca];
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
@@ -1087,7 +1103,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = fmax(bmax, mdp);
       *at(mdr, agent_of(rc[u])) = mdp;
-      *at(Sout, agent_of(rc[u])) = (uint8_t)(own_bits[u] | (dp << 2) | (sn << 4));
+      *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
       if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + spgg_impl::border_slot(r, c, th, tw, HA);
@@ -1672,6 +1688,10 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   }
   int rc = hip_check(c, hipSetDevice(cfg->device), "hipSetDevice");
   if (!rc) rc = build_ring_table(c);
+  if (!rc) {  // + the ring cells' border records
+    c->lds_bytes += (size_t)c->ring_max * spgg_impl::pf_of(cfg->algorithm) * sizeof(double);
+    if (c->lds_bytes > 160 * 1024) rc = fail(c, SPGG_E_ARG, "tile LDS footprint exceeds 160 KB");
+  }
   if (rc) {
     spgg_destroy(c);
     return rc;

@@ -256,3 +256,34 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
                 assert np.array_equal(x, y)
         assert np.array_equal(res[1][2], res[G][2])
         np.testing.assert_allclose(res[1][1], res[G][1], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("M2,state,alg,gain", [
+    (False, "action", "qlearning", 1.0),
+    (True, "reputation", "sarsa", 0.3),            # non-dyadic gain: f64 reputation planes
+    (False, "reputation", "expected_sarsa", 0.3),
+    (True, "action", "double_qlearning", 1.0),
+    (False, "reputation", "double_qlearning", 0.3),
+    (True, "reputation", "qlearning", 1.0),
+])
+def test_compile_time_width_paths_bit_exact(M2, state, alg, gain):
+    """Kernels of compile-time tile width (L % 40 == 0: aligned-dword window staging, one LDS
+    pitch) for every operator, order, state representation and reputation storage."""
+    L, T = 120, 40
+    reps = [_runner_params(seed=s, rep_gain_C=gain, r=3.0 + 0.4 * s) for s in (5, 6)]
+    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng="mt19937",
+                      algorithm=alg)
+    if alg != "double_qlearning":   # Double-Q tiles hold <= 512 agents: run-time width
+        assert eng.tile == (40, 24)
+    eng.run(snapshots=False)
+    for k, p in enumerate(reps):
+        ds, fin = _oracle_final(L, T, p, p.seed, M2, state, algorithm=alg)
+        Q, R, S = eng.final_state(k)
+        assert np.array_equal(S, fin["S"]) and np.array_equal(R, fin["R"]) and np.array_equal(Q, fin["Q"])
+        h = eng.histories()[k]
+        assert np.array_equal(h["coop_rate_history"], ds["coop_rate_history"])
+        assert np.array_equal(h["switch_C_to_D"], ds["switch_C_to_D"])
+        for key in ("neighbor_influence_percent", "avg_q_s0_c_history", "rep_avg_history_final",
+                    "avg_reward_D_history", "rep_component_history"):
+            np.testing.assert_allclose(h[key], ds[key], equal_nan=True, err_msg=key, **FLOAT_TOL)
+    eng.close()

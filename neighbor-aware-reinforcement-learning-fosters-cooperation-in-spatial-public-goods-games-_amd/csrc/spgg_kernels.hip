@@ -88,6 +88,7 @@ struct TileArgs {
 // What a step launch needs to pick and size the kernel instance.
 struct LaunchCfg {
   int m2, as, rq, rng, twc, total_tiles;
+  int apt;  // agents per thread: apt_of(alg), or 1 for small batches
   size_t lds_bytes;
 };
 
@@ -1273,6 +1274,11 @@ template <bool M2, bool AS, bool RQ, int RNG, int ALG>
 void launch_t(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
   constexpr int APT = apt_of(ALG);
   const dim3 grid(((lc.total_tiles + 7) / 8) * 8);
+  if (lc.apt == 1) {  // small batch: one agent per thread (tiles of <= 256 agents, run-time width)
+    hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 1, 0, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a, t,
+                       fin);
+    return;
+  }
 #ifndef SPGG_NO_TWC
   if (lc.twc == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
     hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, APT, 40, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
@@ -1511,6 +1517,13 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
   return fail(c, SPGG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Below this many workgroups per launch (at the operator's agents per thread)
+// a batch runs one agent per thread.  0: never by default -- measured on one
+// L=200 replica the 4x workgroups lose (11.6 vs 10.6 us/step): every workgroup
+// adds its history atomics to the same replica record, 160 per address instead
+// of 40.  The mode stays selectable (SPGG_APT=1) and under test.
+constexpr long long kSmallBatchTiles = 0;
+
 // Tile shape: <= max_agents (256 threads x agents per thread), rows >= 16
 // wide when L allows; minimise padded lanes + halo recompute per agent
 // (L=200 -> 40x25, L=1000 -> 40x25 at 1024 agents).
@@ -1619,6 +1632,7 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   lc.rq = c->cfg.rep_int8 != 0;
   lc.rng = c->cfg.rng_mode;
   lc.twc = twc_of(c->cfg, c->TW, c->TH);
+  lc.apt = c->apt;
   lc.total_tiles = c->cfg.n_rep * c->tiles_per_rep;
   lc.lds_bytes = c->lds_bytes;
   switch (c->cfg.algorithm) {
@@ -1664,7 +1678,20 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   if (!c) return SPGG_E_ARG;
   c->cfg = *cfg;
   c->n = cfg->L * cfg->L;
-  c->apt = spgg_impl::apt_of(cfg->algorithm);
+  // Agents per thread: the operator's maximum (tiles of up to 1024 agents), or
+  // one for a batch that would launch fewer than kSmallBatchTiles workgroups
+  // (4x the workgroups, each a quarter as long); SPGG_APT=1 / =<max> forces either.
+  const int apt_max = spgg_impl::apt_of(cfg->algorithm);
+  c->apt = apt_max;
+  {
+    int tw4, th4;
+    choose_tile(cfg->L, kBlock * apt_max, &tw4, &th4);
+    const long long tiles4 = (long long)cfg->n_rep * ((cfg->L + tw4 - 1) / tw4) * ((cfg->L + th4 - 1) / th4);
+    const char* e = getenv("SPGG_APT");
+    const int forced = e ? atoi(e) : 0;
+    if (forced == 1 || forced == apt_max) c->apt = forced;
+    else if (tiles4 < kSmallBatchTiles) c->apt = 1;
+  }
   choose_tile(cfg->L, kBlock * c->apt, &c->TW, &c->TH);
   if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;

@@ -80,6 +80,13 @@ def _oracle_final(L, T, p, seed, M2, state, algorithm="qlearning"):
     return ds, fin
 
 
+def _force_apt(monkeypatch, apt, alg="qlearning"):
+    """Agents per thread of the step kernel: "1" (small-batch mode) or "max" (4; Double-Q 2)."""
+    if apt == "max":
+        apt = "2" if alg == "double_qlearning" else "4"
+    monkeypatch.setenv("SPGG_APT", apt)
+
+
 def _runner_params(**kw):
     base = dict(c=1, cost=1, alpha=0.8, gamma=0.9, epsilon=0.5, epsilon_decay=0.99,
                 epsilon_min=0.01, lambda_epsilon=0.01, delta_R_D=1, R_min=-10, R_max=10,
@@ -88,8 +95,10 @@ def _runner_params(**kw):
     return ReplicaParams(**base)
 
 
+@pytest.mark.parametrize("apt", ["1", "max"])
 @pytest.mark.parametrize("M2,state", [(False, "reputation"), (True, "action"), (True, "reputation")])
-def test_batched_replicas_match_oracle(M2, state):
+def test_batched_replicas_match_oracle(M2, state, apt, monkeypatch):
+    _force_apt(monkeypatch, apt)
     L, T = 20, 60
     reps = [_runner_params(r=r, influence_factor=k, seed=s)
             for r, k, s in [(2.5, 0.0, 1), (3.0, 1.0, 2), (3.8, 0.5, 3), (5.0, 2.0, 4), (1.0, 1.0, 5)]]
@@ -110,10 +119,12 @@ def test_batched_replicas_match_oracle(M2, state):
 ALGS = ["qlearning", "sarsa", "expected_sarsa", "double_qlearning"]
 
 
+@pytest.mark.parametrize("apt", ["1", "max"])
 @pytest.mark.parametrize("alg", ALGS[1:])
 @pytest.mark.parametrize("M2,state", [(False, "reputation"), (True, "action"), (True, "reputation")])
-def test_batched_operators_match_oracle(alg, M2, state):
+def test_batched_operators_match_oracle(alg, M2, state, apt, monkeypatch):
     """SARSA / Expected SARSA / Double-Q batches, device MT19937, vs the oracle bit for bit."""
+    _force_apt(monkeypatch, apt, alg)
     L, T = 18, 50
     reps = [_runner_params(r=r, influence_factor=k, seed=s)
             for r, k, s in [(2.5, 0.0, 11), (3.0, 1.0, 12), (4.2, 0.5, 13), (1.0, 1.5, 14)]]
@@ -179,8 +190,10 @@ def test_device_mt_stream_matches_numpy(alg):
     eng.close()
 
 
+@pytest.mark.parametrize("apt", ["1", "max"])
 @pytest.mark.parametrize("L,T,M2", [(200, 150, False), (200, 60, True), (1000, 3, False)])
-def test_full_size_bit_exact(L, T, M2):
+def test_full_size_bit_exact(L, T, M2, apt, monkeypatch):
+    _force_apt(monkeypatch, apt)
     p = _runner_params(seed=0)
     eng = BatchEngine(L, T, [p], use_second_order=M2, rng="mt19937")
     eng.run(snapshots=False)
@@ -266,9 +279,10 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
     (False, "reputation", "double_qlearning", 0.3),
     (True, "reputation", "qlearning", 1.0),
 ])
-def test_compile_time_width_paths_bit_exact(M2, state, alg, gain):
+def test_compile_time_width_paths_bit_exact(M2, state, alg, gain, monkeypatch):
     """Kernels of compile-time tile width (L % 40 == 0: aligned-dword window staging, one LDS
     pitch) for every operator, order, state representation and reputation storage."""
+    _force_apt(monkeypatch, "max", alg)
     L, T = 120, 40
     reps = [_runner_params(seed=s, rep_gain_C=gain, r=3.0 + 0.4 * s) for s in (5, 6)]
     eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng="mt19937",
@@ -286,4 +300,24 @@ def test_compile_time_width_paths_bit_exact(M2, state, alg, gain):
         for key in ("neighbor_influence_percent", "avg_q_s0_c_history", "rep_avg_history_final",
                     "avg_reward_D_history", "rep_component_history"):
             np.testing.assert_allclose(h[key], ds[key], equal_nan=True, err_msg=key, **FLOAT_TOL)
+    eng.close()
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_spgg_dropin_max_agents_per_thread(name, tmp_path, monkeypatch):
+    """The reference fixtures again with the large-batch kernels (4 agents per thread; Double-Q 2):
+    small lattices select the one-agent-per-thread kernels by default."""
+    c = Case(name)
+    _force_apt(monkeypatch, "max", c.algorithm)
+    test_spgg_dropin_matches_reference(name, tmp_path)
+
+
+def test_one_agent_per_thread_mode_selectable(monkeypatch):
+    """SPGG_APT=1: tiles of <= 256 agents (one per thread); default: 1000-agent tiles at L=200."""
+    eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
+    assert eng.tile == (40, 25)
+    eng.close()
+    _force_apt(monkeypatch, "1")
+    eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
+    assert eng.tile[0] * eng.tile[1] <= 256
     eng.close()

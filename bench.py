@@ -179,7 +179,7 @@ def main():
     agent_steps = float(executed.sum()) * L * L
 
     # final cooperation-rate gather over RCCL (the path's only collective)
-    ncoop = eng.stats[:, :, 0].cpu().numpy()          # SPGG_ST_NCOOP per iteration slot
+    ncoop = eng.stats_folded()[:, :, 0].cpu().numpy()  # SPGG_ST_NCOOP per iteration slot
     coop = torch.from_numpy(np.array([ncoop[k, int(last[k]) + 1] / (L * L) for k in range(len(reps))]))
     coop = coop.to(torch.device("cuda", local))
     tot = torch.tensor([agent_steps, wall], dtype=torch.float64, device=coop.device)

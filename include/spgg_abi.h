@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 7
+#define SPGG_ABI_VERSION 8
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -56,8 +56,9 @@ extern "C" {
 #define SPGG_RNG_MT19937 1  /* device MT19937, bit-identical to numpy.random.RandomState */
 #define SPGG_RNG_PHILOX 2   /* counter-based Philox2x32-10 keyed by (seed, replica), counter (agent, step) */
 
-/* Per-step history record: stats[rep][t][SPGG_NSTAT] (float64), t = 0 .. iterations+1.
- * Integer counts are stored exactly as float64. */
+/* Per-step history record: stats[rep][stripe][t][SPGG_NSTAT] (float64), t = 0 ..
+ * iterations+1, stripe = 0 .. spgg_stat_stripes()-1.  A slot's value is the SUM of its
+ * stripes, except SPGG_ST_GMAX: the MAX.  Integer counts are stored exactly as float64. */
 enum {
   SPGG_ST_NCOOP = 0,      /* #S_t==0 at iteration start (spgg.py:383)            */
   SPGG_ST_SUMP = 1,       /* sum P                       (spgg.py:388)            */
@@ -163,8 +164,9 @@ typedef struct {
  *                                    is at draws + p*draw_plane_stride + rep*n
  *   mt_state  uint32 [n_rep][625]    MT19937 key[624] + pos (MT19937 only)
  *   eps       f64    [n_rep][iterations+2]  eps used by iteration t
- *   stats     f64    [n_rep][iterations+2][SPGG_NSTAT]  zero-initialised; slot
- *                                    t0 must hold NCOOP of S_t0 before stepping
+ *   stats     f64    [n_rep][stripes][iterations+2][SPGG_NSTAT]  zero-initialised;
+ *                                    stripe 0 of slot t0 must hold NCOOP of S_t0 before
+ *                                    stepping (stripes: spgg_stat_stripes)
  *   stop_iter int32  [n_rep]         0 while running, else the absorbing iteration
  * Initial state: S[0] = population (bits 1-7 zero), R[0] = 0, Q = initial table.
  * Final state of a replica absorbed at s: S, R in [(s-1)&1]; of a replica still
@@ -215,6 +217,11 @@ int spgg_payoff(spgg_ctx* ctx, int32_t t, double* out, void* hip_stream);
 
 /* Doubles per replica of each border-record buffer (spgg_buffers.pub). */
 int spgg_pub_doubles(const spgg_ctx* ctx, int64_t* per_rep);
+
+/* History-record stripes per replica the stats buffer must hold (1 for small
+ * lattices; up to 32 so that <= 64 workgroups add to one record address per
+ * iteration).  Replaces: nothing (reference's per-step np.mean calls). */
+int spgg_stat_stripes(const spgg_ctx* ctx, int32_t* stripes);
 
 /* Tile shape (agents) the step kernel uses for this lattice. */
 int spgg_tile_shape(const spgg_ctx* ctx, int32_t* tw, int32_t* th);

@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -33,7 +33,7 @@ NSTAT = 34
 
 EXPORTED = ("spgg_abi_version", "spgg_last_error", "spgg_create", "spgg_set_params",
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
-            "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles")
+            "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes")
 
 
 class Config(ctypes.Structure):
@@ -107,6 +107,8 @@ def load(path: str | None = None):
         lib.spgg_destroy.argtypes = [vp]
         lib.spgg_draw_planes.restype = ctypes.c_int
         lib.spgg_draw_planes.argtypes = [i32]
+        lib.spgg_stat_stripes.restype = ctypes.c_int
+        lib.spgg_stat_stripes.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
         lib.spgg_pub_doubles.restype = ctypes.c_int
         lib.spgg_pub_doubles.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         v = lib.spgg_abi_version()

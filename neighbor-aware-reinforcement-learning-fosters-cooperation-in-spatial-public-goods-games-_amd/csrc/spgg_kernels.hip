@@ -76,13 +76,14 @@ struct TileArgs {
   const uint8_t* draws;   // draw planes (INJECT / MT19937), plane stride `plane`
   size_t plane;
   const double* eps;
-  double* stats;
+  double* stats;          // [rep][stripe][slot][NSTAT]: a workgroup adds to stripe tile % stripes
   int* stop_iter;
   const spgg_rep_params* params;
   const int2* ring;       // [tiles_per_rep][ring_max]: {agent index, border-record offset}
   int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
   int PB;                 // border-record slots per tile (pub_slots)
   int ring_max;
+  int stripes;            // history-record stripes per replica (spgg_stat_stripes)
 };
 
 // What a step launch needs to pick and size the kernel instance.
@@ -838,14 +839,23 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
   }
   const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
-  double* srow = a.stats + (size_t)rep * a.slots * SPGG_NSTAT;
+  // the replica's history record: slot values are sums over its stripes (max for GMAX);
+  // this workgroup adds to stripe tile % stripes (bounded atomic contention per address)
+  const size_t stripe_len = (size_t)a.slots * SPGG_NSTAT;
+  const double* rrow = a.stats + (size_t)rep * a.stripes * stripe_len;
+  double* srow = a.stats + ((size_t)rep * a.stripes + tile % a.stripes) * stripe_len;
   bool stop_now = false;
   if (!fin_only) {
-    const double nc = srow[(size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
+    double nc = 0.0;
+    for (int k = 0; k < a.stripes; ++k) nc += rrow[k * stripe_len + (size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
     stop_now = (nc == 0.0) || (nc == (double)n);  // spgg.py:405
   }
   const bool acting = !fin_only && !stop_now;
-  const double lam_den = pending ? srow[(size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX] + pg.lambda_eps : 1.0;
+  double gmax_prev = 0.0;
+  if (pending)
+    for (int k = 0; k < a.stripes; ++k)
+      gmax_prev = fmax(gmax_prev, rrow[k * stripe_len + (size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX]);
+  const double lam_den = pending ? gmax_prev + pg.lambda_eps : 1.0;
   const double lam_rcp = 1.0 / lam_den;  // IEEE, once per workgroup
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
   const uint64_t eps53 = u53_threshold(eps_t);  // rand < eps_t as an integer compare
@@ -1404,13 +1414,14 @@ __host__ __device__ inline int draw_planes(int alg) {
 
 __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
     uint32_t* mt_state, uint8_t* draws, size_t plane, const double* eps, const double* stats,
-    const int* stop_iter, int n, int slots, int t, int alg) {
+    const int* stop_iter, int n, int slots, int t, int alg, int stripes) {
   __shared__ uint32_t mt[624];
   __shared__ uint32_t carry;
   const int rep = blockIdx.x;
   const int st = stop_iter[rep];
   if (st != 0 && st < t) return;
-  const double nc = stats[((size_t)rep * slots + t) * SPGG_NSTAT + SPGG_ST_NCOOP];
+  double nc = 0.0;  // NCOOP of S_t: the sum over the replica's record stripes
+  for (int k = 0; k < stripes; ++k) nc += stats[(((size_t)rep * stripes + k) * slots + t) * SPGG_NSTAT + SPGG_ST_NCOOP];
   if (nc == 0.0 || nc == (double)n) return;  // absorbing: no draw this iteration
   uint32_t* gstate = mt_state + (size_t)rep * 625;
   const int tid = threadIdx.x;
@@ -1494,6 +1505,7 @@ struct spgg_ctx {
   int ring_max = 0;
   int n = 0;
   int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4, PB = 0;
+  int stripes = 1;  // history-record stripes per replica
   size_t lds_bytes = 0;
   std::string err;
 };
@@ -1523,6 +1535,9 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
 // adds its history atomics to the same replica record, 160 per address instead
 // of 40.  The mode stays selectable (SPGG_APT=1) and under test.
 constexpr long long kSmallBatchTiles = 0;
+
+// Workgroups per history-record stripe (spgg_stat_stripes).
+constexpr int kTilesPerStripe = 64;
 
 // Tile shape: <= max_agents (256 threads x agents per thread), rows >= 16
 // wide when L allows; minimise padded lanes + halo recompute per agent
@@ -1621,6 +1636,7 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   a.PB = c->PB;
   a.ring = c->d_ring;
   a.ring_max = c->ring_max;
+  a.stripes = c->stripes;
   return a;
 }
 
@@ -1646,7 +1662,8 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
 void launch_draw(const spgg_ctx* c, int t, hipStream_t s) {
   hipLaunchKernelGGL(spgg_mt_draw_kernel, dim3(c->cfg.n_rep), dim3(kMtThreads), 0, s,
                      c->buf.mt_state, c->buf.draws, (size_t)c->buf.draw_plane_stride, c->buf.eps,
-                     c->buf.stats, c->buf.stop_iter, c->n, c->cfg.iterations + 2, t, c->cfg.algorithm);
+                     c->buf.stats, c->buf.stop_iter, c->n, c->cfg.iterations + 2, t, c->cfg.algorithm,
+                     c->stripes);
 }
 
 }  // namespace
@@ -1703,6 +1720,9 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   }
   c->tiles_x = (cfg->L + c->TW - 1) / c->TW;
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
+  // history-record stripes: <= kTilesPerStripe workgroups add to one record address per
+  // iteration (a single record of an L=1000 replica took 1000 atomics per address: ~12 us)
+  while (c->stripes < 32 && (c->tiles_per_rep + c->stripes - 1) / c->stripes > kTilesPerStripe) c->stripes *= 2;
   const int HA = cfg->second_order ? 2 : 1;
   const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8, twc_of(*cfg, c->TW, c->TH) > 0);
   c->lds_bytes = (size_t)ly.bytes;
@@ -1807,6 +1827,12 @@ int spgg_payoff(spgg_ctx* c, int32_t t, double* out, void* stream) {
 int spgg_pub_doubles(const spgg_ctx* c, int64_t* per_rep) {
   if (!c || !per_rep) return SPGG_E_ARG;
   *per_rep = (int64_t)c->tiles_per_rep * spgg_impl::pf_of(c->cfg.algorithm) * c->PB;
+  return SPGG_OK;
+}
+
+int spgg_stat_stripes(const spgg_ctx* c, int32_t* stripes) {
+  if (!c || !stripes) return SPGG_E_ARG;
+  *stripes = c->stripes;
   return SPGG_OK;
 }
 

@@ -254,9 +254,8 @@ class BatchEngine:
             eps[k] = cache[key]
         self.eps_host = eps
         self.eps = torch.from_numpy(eps).to(d)
-        self.stats = torch.zeros((R, T + 2, C.NSTAT), dtype=f64, device=d)
-        ncoop = (S0 == 0).sum(axis=1).astype(np.float64)
-        self.stats[:, 1, C.ST_NCOOP] = torch.from_numpy(ncoop).to(d)
+        # history record [R][stripes][T+2][NSTAT]: allocated in _create (stripes per the library)
+        self._ncoop0 = (S0 == 0).sum(axis=1).astype(np.float64)
         self.stop_iter = torch.zeros(R, dtype=torch.int32, device=d)
         self.P_buf = torch.zeros((R, n), dtype=f64, device=d)
 
@@ -277,10 +276,16 @@ class BatchEngine:
             C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
             arr = (C.RepParams * (r1 - r0))(*params[r0:r1])
             C.check(self.lib.spgg_set_params(ctx, arr), ctx, "spgg_set_params")
-            if g == 0:   # border records: library-defined size per replica
+            if g == 0:   # border records and history-record stripes: library-defined sizes
                 per = ctypes.c_int64()
                 C.check(self.lib.spgg_pub_doubles(ctx, ctypes.byref(per)), ctx, "spgg_pub_doubles")
                 self.pub = torch.zeros((2, self.R, max(1, per.value)), dtype=torch.float64, device=self.dev)
+                ns = ctypes.c_int32()
+                C.check(self.lib.spgg_stat_stripes(ctx, ctypes.byref(ns)), ctx, "spgg_stat_stripes")
+                self.stripes = int(ns.value)
+                self.stats = torch.zeros((self.R, self.stripes, self.T + 2, C.NSTAT), dtype=torch.float64,
+                                         device=self.dev)
+                self.stats[:, 0, 1, C.ST_NCOOP] = torch.from_numpy(self._ncoop0).to(self.dev)
             b = C.Buffers()   # the group's replica slice of every buffer
             for i in range(2):
                 b.S[i], b.R[i] = self.S[i][r0].data_ptr(), self.Rep[i][r0].data_ptr()
@@ -337,7 +342,7 @@ class BatchEngine:
         execute it: every select draws rand then randint (algorithms.py:105,108);
         SARSA selects three times (spgg.py:410,434,452); Double-Q then draws its
         table choice (algorithms.py:302)."""
-        ncoop = self.stats[:, t, C.ST_NCOOP].cpu().numpy()
+        ncoop = self.stats[:, :, t, C.ST_NCOOP].sum(dim=1).cpu().numpy()
         stop = self.stop_iter.cpu().numpy()
         planes = np.zeros((self.n_planes, self.R, self.n), dtype=np.uint8)
         L = self.L
@@ -466,18 +471,25 @@ class BatchEngine:
             self.lib.spgg_payoff(g["ctx"], int(t), self.P_buf[g["r0"]].data_ptr(), s), g["ctx"], "spgg_payoff"))
         return self.P_buf.cpu().numpy().reshape(self.R, self.L, self.L)
 
+    def stats_folded(self):
+        """(R, T+2, NSTAT) device tensor of the history record: stripes summed, GMAX maxed."""
+        st = self.stats.sum(dim=1)
+        if self.stripes > 1:
+            st[..., C.ST_GMAX] = self.stats[..., C.ST_GMAX].amax(dim=1)
+        return st
+
     def mt_state_host(self, k):
         st = self.mt_state[k].cpu().numpy().view(np.uint32)
         return st[:624].copy(), int(st[624])
 
     def histories(self):
         """Per-replica dict of the reference's per-iteration datasets (spgg.py:595-618)."""
-        st = self.stats.cpu().numpy()
+        st = self.stats_folded().cpu().numpy()
         return [histories_from_stats(st[k], self.last_iteration(k), int(self.stopped[k]) != 0,
                                      self.eps_host[k], self.n) for k in range(self.R)]
 
     def gmax_history(self, k):
-        st = self.stats[k, :, C.ST_GMAX].cpu().numpy()
+        st = self.stats_folded()[k, :, C.ST_GMAX].cpu().numpy()
         last = self.last_iteration(k)
         m = last - 1 if int(self.stopped[k]) else last
         return st[1:m + 1]

@@ -1,0 +1,49 @@
+"""The C-ABI library (CPU-side checks only, no device calls): it loads, reports the
+header's ABI version, and exports every function include/spgg_abi.h declares -- the
+set the ctypes binding types (spgg_amd/_lib.py EXPORTED)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from spgg_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "spgg_abi.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(spgg_\w+)\s*\(", src, flags=re.M))
+
+
+def test_header_declares_the_bound_functions():
+    assert _declared() == set(_lib.EXPORTED)
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [name for name in sorted(_declared()) if not hasattr(lib, name)]
+    assert not missing, missing
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_abi_version_matches_header():
+    v = int(re.search(r"#define SPGG_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    lib = _lib.load()
+    assert lib.spgg_abi_version() == v == _lib.ABI_VERSION
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_argument_errors_without_device():
+    """Null arguments fail with SPGG_E_ARG before any device call."""
+    lib = _lib.load()
+    assert lib.spgg_create(None, None) == _lib.E_ARG
+    assert lib.spgg_step(None, 1, 1, None) == _lib.E_ARG
+    assert lib.spgg_draw_planes(7) == _lib.E_ARG
+    assert lib.spgg_draw_planes(_lib.ALG_SARSA) == 6
+    n = ctypes.c_int32()
+    assert lib.spgg_stat_stripes(None, ctypes.byref(n)) == _lib.E_ARG
+    assert lib.spgg_destroy(None) == _lib.OK

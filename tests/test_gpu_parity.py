@@ -174,7 +174,7 @@ def test_device_mt_stream_matches_numpy(alg):
     reference_init(L, rs, algorithm=alg)
     lib = eng.lib
     from spgg_amd import _lib as C
-    eng.stats[:, :, C.ST_NCOOP] = 1.0   # no iteration is absorbing: every draw happens
+    eng.stats[:, 0, :, C.ST_NCOOP] = 1.0   # no iteration is absorbing: every draw happens
     for t in (1, 2, 3):
         C.check(lib.spgg_draw(eng.ctx, t, eng.stream), eng.ctx, "spgg_draw")
         d = O.draw_step(rs, L, alg)
@@ -260,7 +260,7 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
         eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=G, algorithm=alg)
         assert eng.G == G
         eng.run(snapshots=False)
-        res[G] = ([eng.final_state(k) for k in range(len(reps))], eng.stats.cpu().numpy(),
+        res[G] = ([eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy(),
                   eng.stop_iter.cpu().numpy())
         eng.close()
     for G in (3, 4):
@@ -320,4 +320,24 @@ def test_one_agent_per_thread_mode_selectable(monkeypatch):
     _force_apt(monkeypatch, "1")
     eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
     assert eng.tile[0] * eng.tile[1] <= 256
+    eng.close()
+
+
+def test_history_record_stripes_l1000(monkeypatch):
+    """An L=1000 replica spreads its history atomics over stripes (<= 64 tiles per stripe);
+    the folded record still matches the oracle (integer counts exact)."""
+    L, T = 1000, 3
+    p = _runner_params(seed=1)
+    eng = BatchEngine(L, T, [p], use_second_order=False, rng="mt19937")
+    assert eng.stripes == 16
+    eng.run(snapshots=False)
+    ds, fin = _oracle_final(L, T, p, 1, False, "reputation")
+    h = eng.histories()[0]
+    for key in ("coop_rate_history", "switch_C_to_D", "switch_D_to_C", "group_comp_d2_history"):
+        assert np.array_equal(h[key], ds[key]), key
+    for key in ("neighbor_influence_percent", "avg_q_s0_c_history", "it_records_final"):
+        np.testing.assert_allclose(h[key], ds[key], err_msg=key, **FLOAT_TOL)
+    np.testing.assert_array_equal(eng.gmax_history(0) > 0, True)
+    Q, R, S = eng.final_state(0)
+    assert np.array_equal(Q, fin["Q"]) and np.array_equal(S, fin["S"])
     eng.close()

@@ -46,7 +46,8 @@ using namespace spgg;
 // Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
-//   128 = memory only (the owned loads, staging and stores, no compute)
+//   16 = no workgroup totals (final barrier + epilogue), 128 = memory only (the owned loads,
+//   staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
@@ -1150,6 +1151,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   {  // the tile's max(0, max_diff): wave maxima -> red[wave*64 + 12]
     const double wm = wave_max(bmax);
     if ((tid & 63) == 0) red[(tid >> 6) * 64 + 12] = wm;
+  }
+  if (SPGG_ABLATE & 16) {  // timing probe: no workgroup totals (barrier + epilogue); NCOOP kept constant
+    if (tid == 0 && tile == 0 && acting) srow[(size_t)(t + 1) * SPGG_NSTAT] = n / 2;
+    return;
   }
   __syncthreads();
   STAMP(6);

@@ -69,3 +69,29 @@ def test_run_one_experiment_dropin(tmp_path, monkeypatch):
     assert params == p7 and 0.0 <= coop <= 1.0 and rep_mean == 0
     fn = tmp_path / sweep.get_folder_name(*p7) / "data" / "experiment_data.h5"
     assert "coop_rate_history" in read_datasets(str(fn))
+
+
+def test_figures_regenerate_from_gpu_sweep(tmp_path, monkeypatch):
+    """SURVEY §8f rank 4 end to end: the reference's paper-figure grid
+    (all_figures + the state comparison pair) swept on the GPU, then every
+    figure of scripts/plot_figures.py / plot_state_comparison.py regenerated
+    from the files the sweep wrote."""
+    from spgg_amd import figures
+    monkeypatch.chdir(tmp_path)
+    tuples = sweep.generate_param_combinations(sweep.DEFAULT_CONFIG, "all_figures")
+    tuples += [(4.6, 0.0, False, 0.8, 1.0, 1.0, st) for st in ("reputation", "action")]
+    small = dict(L=16, iterations=120)
+    res = sweep.run_experiments(tuples, use_progress_bar=False, seeds=list(range(len(tuples))),
+                                devices=[0], save_png=False, **small)
+    assert len(res) == len(tuples)
+    out = figures.plot_figures(str(tmp_path), str(tmp_path / "figs"), ["all"], total_iterations=120)
+    assert sorted(out) == list(figures.FIGURES)
+    for path in out.values():
+        assert os.path.getsize(path) > 1000, path
+    sc = figures.state_comparison(str(tmp_path), str(tmp_path / "figs"), total_iterations=121)
+    assert os.path.getsize(sc) > 1000
+    # every curve of Figure 2 is a file's coop_rate_history
+    for k, paths in figures.figure_inputs(str(tmp_path))["2"].items():
+        for p in paths.values():
+            h = figures.load_data(p, "coop_rate_history")
+            assert h is not None and 1 <= len(h) <= 120 and np.all((h >= 0) & (h <= 1))

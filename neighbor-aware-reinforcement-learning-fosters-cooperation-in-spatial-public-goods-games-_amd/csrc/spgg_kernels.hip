@@ -51,6 +51,12 @@ using namespace spgg;
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
+#ifndef SPGG_PRIO
+#define SPGG_PRIO 0  // wave priority while a workgroup issues its loads (0: off)
+#endif
+#ifndef SPGG_PRIO_LATE
+#define SPGG_PRIO_LATE 0  // 1: priority 1 from phase 1b, 2 from phase 2; 2: priority 2 from phase 2
+#endif
 
 // Build layout: this file is compiled once per RL operator with
 // -DSPGG_TU=<SPGG_ALG_*> (that operator's step kernels only) and once with
@@ -739,6 +745,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const bool pending = t > 1;
   const int tid = threadIdx.x;
   const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
+  if (SPGG_PRIO) __builtin_amdgcn_s_setprio(SPGG_PRIO);
   STAMP(0);
 #if SPGG_STAMPS
   if (t == SPGG_STAMP_T && tid == 0 && logical < kStampWG) {
@@ -864,6 +871,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
                         (uint32_t)pg.stream_id * 0xC2B2AE35u;
 
+  if (SPGG_PRIO) __builtin_amdgcn_s_setprio(0);
   // windows -> LDS (waits for the loads above)
   if constexpr (TWC > 0) {
     winS.store(sS, ly.sw, th + 2 * HS, sD);
@@ -965,6 +973,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
   }
   STAMP(2);
+  if (SPGG_PRIO_LATE == 1) __builtin_amdgcn_s_setprio(1);
   __syncthreads();  // plus counts and ring records complete
 
   // ---- phase 1b: iteration start + action select for owned agents --------
@@ -1075,6 +1084,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   }
   __syncthreads();
   STAMP(4);
+  if (SPGG_PRIO_LATE) __builtin_amdgcn_s_setprio(2);
 
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;

@@ -226,6 +226,37 @@ def test_philox_mode_deterministic_and_sane():
         assert h["epsilon_history_final"][0] == max(0.5 * 0.99, 0.01)
 
 
+@pytest.mark.parametrize("kappa,M2", [(1.0, False), (0.0, False), (1.0, True)])
+def test_philox_statistical_parity(kappa, M2):
+    """The bench's Philox stream against the reference's MT19937 stream at the
+    bench's lattice size (L=200): ensembles of 12 replicas per stream, same init
+    law, must agree in the mean cooperation rate, the mean switch counts and the
+    mean NI share at every checkpoint within 5 standard errors of the difference
+    (+ 2e-3 absolute for near-deterministic phases).  Statistical parity is what
+    the bench's number rests on."""
+    L, T, n = 200, 200, 12
+    runs = {}
+    for rng, base in (("mt19937", 0), ("philox", 1000)):
+        reps = [_runner_params(seed=base + s, influence_factor=kappa, r=3.6, reward_weight_payoff=1.0)
+                for s in range(n)]
+        eng = BatchEngine(L, T, reps, use_second_order=M2, rng=rng)
+        eng.run(snapshots=False)
+        hs = eng.histories()
+        eng.close()
+        runs[rng] = hs
+    for key in ("coop_rate_history", "switch_C_to_D", "switch_D_to_C", "neighbor_influence_percent"):
+        def pad(x):  # an absorbed replica stops early: hold its rate, no switches after
+            x = np.asarray(x, dtype=np.float64)[:T - 1]
+            fill = x[-1] if key == "coop_rate_history" and len(x) else 0.0
+            return np.concatenate([x, np.full(T - 1 - len(x), fill)])
+        a = np.stack([pad(h[key]) for h in runs["mt19937"]])
+        b = np.stack([pad(h[key]) for h in runs["philox"]])
+        for t in (0, 9, 49, 99, T - 2):
+            se = np.sqrt(a[:, t].var(ddof=1) / n + b[:, t].var(ddof=1) / n)
+            tol = 5 * se + 2e-3 * max(1.0, abs(a[:, t].mean()))
+            assert abs(a[:, t].mean() - b[:, t].mean()) <= tol, (key, t, a[:, t].mean(), b[:, t].mean(), se)
+
+
 @pytest.mark.parametrize("name", ["m1_rep_L16", "m2_rep_L24_stopC", "defaults_L12", "m2_act_L13_odd"])
 def test_spgg_dropin_f64_reputation_path(name, tmp_path, monkeypatch):
     """Same fixtures with the compact int8 reputation disabled (f64 R planes)."""

@@ -535,14 +535,32 @@ __device__ __forceinline__ int draw_table1(const TileArgs& a, size_t rb, int g, 
   }
 }
 
+// Per-agent streams (Q, md, atd): read once and written once per iteration.
+// SPGG_NT=1 marks them non-temporal (measurement knob: keeps them from
+// displacing the halo windows and border records other tiles re-read in L2).
+#ifndef SPGG_NT
+#define SPGG_NT 0
+#endif
+typedef double vd2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (SPGG_NT != 0) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+  if constexpr (SPGG_NT != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <int QB>
 __device__ __forceinline__ void load_q(const double* Qr, uint32_t agent, double (&q)[4],
                                        double (&qb)[QB ? 4 : 1]) {
-  const double2* qp = at(reinterpret_cast<const double2*>(Qr), agent * (QB ? 4 : 2));
-  const double2 q01 = qp[0], q23 = qp[1];
+  const vd2* qp = at(reinterpret_cast<const vd2*>(Qr), agent * (QB ? 4 : 2));
+  const vd2 q01 = ld_stream(qp), q23 = ld_stream(qp + 1);
   q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
   if constexpr (QB) {
-    const double2 b01 = qp[2], b23 = qp[3];
+    const vd2 b01 = ld_stream(qp + 2), b23 = ld_stream(qp + 3);
     qb[0] = b01.x; qb[1] = b01.y; qb[2] = b23.x; qb[3] = b23.y;
   }
 }
@@ -550,12 +568,12 @@ __device__ __forceinline__ void load_q(const double* Qr, uint32_t agent, double 
 template <int QB>
 __device__ __forceinline__ void store_q(double* Qr, uint32_t agent, const double (&q)[4],
                                         const double (&qb)[QB ? 4 : 1]) {
-  double2* qo = at(reinterpret_cast<double2*>(Qr), agent * (QB ? 4 : 2));
-  qo[0] = make_double2(q[0], q[1]);
-  qo[1] = make_double2(q[2], q[3]);
+  vd2* qo = at(reinterpret_cast<vd2*>(Qr), agent * (QB ? 4 : 2));
+  st_stream(qo, vd2{q[0], q[1]});
+  st_stream(qo + 1, vd2{q[2], q[3]});
   if constexpr (QB) {
-    qo[2] = make_double2(qb[0], qb[1]);
-    qo[3] = make_double2(qb[2], qb[3]);
+    st_stream(qo + 2, vd2{qb[0], qb[1]});
+    st_stream(qo + 3, vd2{qb[2], qb[3]});
   }
 }
 
@@ -791,8 +809,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       // conditional loads serialise on each other
       const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0);
       load_q<QB>(Qr, g, q[u], qb[u]);
-      md_own[u] = *at(mdr, g);
-      atd_own[u] = *at(atdr, g);
+      md_own[u] = ld_stream(at(mdr, g));
+      atd_own[u] = ld_stream(at(atdr, g));
       r += dr;
       c += dc;
       if (c >= tw) {
@@ -1103,7 +1121,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
       const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
                                             act, sn, q[u], qb[u]);
-      if (kappa != 0.0) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
+      if (kappa != 0.0) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
       store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
@@ -1124,7 +1142,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = fmax(bmax, mdp);
-      *at(mdr, agent_of(rc[u])) = mdp;
+      st_stream(at(mdr, agent_of(rc[u])), mdp);
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
       if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring

@@ -211,13 +211,14 @@ def main():
             "data": "synthetic (reference init: S~Bernoulli(1/2), R=0, Q~U(-0.01,0.01))",
             "config": {"workload": desc, "L": L, "replicas_per_gpu": len(reps),
                        "agents_per_gpu": n_agents, "second_order": M2, "state": state,
-                       "rng": args.rng, "streams_per_gpu": eng.G,
+                       "rng": args.rng, "streams_per_gpu": eng.resident, "replica_groups": eng.G,
+                       "cache_waves": eng.waves,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes per iteration (all replicas), from profiles/r01/current/traffic_*.json",
                          "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
-                         "kernel": (f"spgg_step_kernel, {eng.G} concurrent launches per iteration "
+                         "kernel": (f"spgg_step_kernel, {eng.resident} concurrent launches per iteration "
                                     f"(one per replica group/stream)" if args.rng == "philox" else
                                     "spgg_mt_draw_kernel + spgg_step_kernel per replica group"),
                          "device_ms_per_step": per_step_dev_s * 1e3},

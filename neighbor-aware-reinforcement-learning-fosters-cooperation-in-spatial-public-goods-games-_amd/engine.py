@@ -190,9 +190,19 @@ class BatchEngine:
         # Replica groups on separate HIP streams: their step kernels run
         # concurrently, so one group's tail / compute phase overlaps another
         # group's memory phase (a single launch moves in lockstep rounds).
+        # Infinity-Cache blocking: a batch whose state exceeds the cache budget is
+        # stepped in `waves` turns -- the groups of one wave run concurrently (one
+        # stream each) for `chunk` iterations while the next wave's groups queue
+        # behind them on the same streams (groups are independent: results are
+        # unchanged, only the order of launches across groups)
+        self.cache_bytes = int(float(os.environ.get("SPGG_CACHE_MB", "240")) * 2**20)
+        self.chunk = max(1, int(os.environ.get("SPGG_CHUNK", "64")))
+        total = self.state_bytes_per_replica() * self.R
+        self.waves = 1 if rng == "inject" else int(max(1, min(self.R, -(-total // self.cache_bytes))))
         if streams is None:
             streams = int(os.environ.get("SPGG_STREAMS", "0")) or self._auto_streams()
         self.G = 1 if rng == "inject" else max(1, min(int(streams), self.R))
+        self.resident = self.G if self.waves == 1 else max(1, -(-self.G // self.waves))
         self._alloc()
         self._create()
         self.t = 1                 # next iteration to execute
@@ -202,12 +212,22 @@ class BatchEngine:
         self._flushed = False
 
     def _auto_streams(self):
-        """~1400 workgroups per group kernel (measured best on MI355X for cfg3: 3 groups
-        78 us/step vs 6 groups 86); small batches stay on one stream (cross-stream
-        ordering costs more than it hides)."""
+        """Replica groups: ~1400 workgroups per group kernel (measured best on MI355X for
+        cfg3: 3 groups 78 us/step vs 6 groups 86), at most 8 concurrent; small batches
+        stay in one group (cross-stream ordering costs more than it hides).  With cache
+        blocking, that many groups per wave."""
         tw = min(self.L, 40)
         tiles = -(-self.L // tw) * -(-self.L // min(self.L, 25))
-        return int(max(1, min(8, round(self.R * tiles / 1400))))
+        per_wave = int(max(1, min(8, round(self.R / self.waves * tiles / 1400))))
+        return per_wave * self.waves if self.waves > 1 else per_wave
+
+    def state_bytes_per_replica(self) -> int:
+        """Bytes of per-agent state one iteration reads and writes (Q, md, atd, the
+        S / R ping-pong, ~10 % border records): the Infinity-Cache working set.
+        Budget SPGG_CACHE_MB (default 240 of the MI355X's 256 MB: measured knee for
+        L=200 between 227 and 272 MB, profiles/r01/current/replicas_sweep_*)."""
+        rsz = 1 if all(p.rep_unit() is not None for p in self.reps) else 8
+        return int(self.n * (self.QW * 8 + 8 + 4 + 2 + 2 * rsz) * 1.1)
 
     # -- setup ---------------------------------------------------------------
     def _alloc(self):
@@ -268,6 +288,10 @@ class BatchEngine:
         for k, p in enumerate(params):
             p.stream_id = k
         self.groups = []
+        if self.G == 1:
+            streams = [torch.cuda.current_stream(self.dev)]
+        else:
+            streams = [torch.cuda.Stream(self.dev) for _ in range(self.resident)]
         bounds = np.linspace(0, self.R, self.G + 1).round().astype(int)
         for g in range(self.G):
             r0, r1 = int(bounds[g]), int(bounds[g + 1])
@@ -297,26 +321,30 @@ class BatchEngine:
             b.eps, b.stats = self.eps[r0].data_ptr(), self.stats[r0].data_ptr()
             b.stop_iter = self.stop_iter[r0].data_ptr()
             C.check(self.lib.spgg_bind(ctx, b), ctx, "spgg_bind")
-            stream = torch.cuda.current_stream(self.dev) if self.G == 1 else torch.cuda.Stream(self.dev)
-            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, bufs=b, stream=stream))
+            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, bufs=b, stream=streams[g % len(streams)]))
+        self.streams = streams
         self.ctx = self.groups[0]["ctx"]
         tw, th = ctypes.c_int32(), ctypes.c_int32()
         C.check(self.lib.spgg_tile_shape(self.ctx, ctypes.byref(tw), ctypes.byref(th)), self.ctx, "tile")
         self.tile = (tw.value, th.value)
 
-    def _enqueue(self, fn):
-        """Run fn(group, stream_handle) on every group's stream, ordered after the
-        current stream's prior work and before its later work."""
+    def _enqueue(self, fn, rounds=(None,)):
+        """For each round, run fn(group, stream_handle[, round]) on every group's
+        stream, all ordered after the current stream's prior work and before its
+        later work.  Groups sharing a stream (cache blocking) run in turn."""
         cur = torch.cuda.current_stream(self.dev)
+        call = (lambda g, s, r: fn(g, s)) if rounds == (None,) else fn
         if self.G == 1:
-            fn(self.groups[0], cur.cuda_stream)
+            for r in rounds:
+                call(self.groups[0], cur.cuda_stream, r)
             return
-        for g in self.groups:
-            g["stream"].wait_stream(cur)
-        for g in self.groups:
-            fn(g, g["stream"].cuda_stream)
-        for g in self.groups:
-            cur.wait_stream(g["stream"])
+        for st in self.streams:
+            st.wait_stream(cur)
+        for r in rounds:
+            for g in self.groups:
+                call(g, g["stream"].cuda_stream, r)
+        for st in self.streams:
+            cur.wait_stream(st)
 
     def close(self):
         for g in getattr(self, "groups", []):
@@ -369,9 +397,13 @@ class BatchEngine:
                 C.check(self.lib.spgg_step(self.ctx, self.t, 1, self.stream), self.ctx, "spgg_step")
                 self.t += 1
         else:
-            t0 = self.t
-            self._enqueue(lambda g, s: C.check(self.lib.spgg_step(g["ctx"], t0, n_steps, s), g["ctx"],
-                                               "spgg_step"))
+            t0, end = self.t, self.t + n_steps
+            if self.resident >= self.G:   # every group resident: one enqueue per group
+                chunks = [(t0, n_steps)]
+            else:                         # cache blocking: groups take turns, chunk iterations each
+                chunks = [(t, min(self.chunk, end - t)) for t in range(t0, end, self.chunk)]
+            self._enqueue(lambda g, s, c: C.check(self.lib.spgg_step(g["ctx"], c[0], c[1], s), g["ctx"],
+                                                  "spgg_step"), rounds=chunks)
             self.t += n_steps
         return n_steps
 

@@ -302,6 +302,37 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
         np.testing.assert_allclose(res[1][1], res[G][1], rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("rng", ["philox", "mt19937"])
+def test_cache_blocked_waves_match_concurrent_groups(rng, monkeypatch):
+    """Infinity-Cache blocking (groups take turns on shared streams, chunk
+    iterations at a time) only reorders launches across independent groups:
+    bit-identical to every group resident at once, including a chunk that does
+    not divide the step counts and absorbing stops inside a chunk."""
+    L, T = 30, 61
+    reps = [_runner_params(r=1.5 + 0.4 * s, influence_factor=0.5 * (s % 3), seed=40 + s) for s in range(10)]
+    res = {}
+    for mode in ("resident", "waves"):
+        if mode == "waves":
+            monkeypatch.setenv("SPGG_CACHE_MB", "0.2")   # 10 x ~48 KB of state: 3 waves
+            monkeypatch.setenv("SPGG_CHUNK", "7")
+        eng = BatchEngine(L, T, reps, use_second_order=True, rng=rng, streams=6)
+        if mode == "waves":
+            assert eng.waves == 3 and eng.G == 6 and eng.resident == 2, (eng.waves, eng.G, eng.resident)
+        else:
+            assert eng.waves == 1 and eng.resident == eng.G == 6
+        for n in (5, 20, 36):   # uneven step() calls, as SPGG.run's snapshot stops make them
+            eng.step(n)
+        eng.flush()
+        res[mode] = ([eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy(),
+                     eng.stop_iter.cpu().numpy())
+        eng.close()
+    for a, b in zip(res["resident"][0], res["waves"][0]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    assert np.array_equal(res["resident"][2], res["waves"][2])
+    np.testing.assert_allclose(res["resident"][1], res["waves"][1], rtol=1e-12, atol=1e-12)
+
+
 @pytest.mark.parametrize("M2,state,alg,gain", [
     (False, "action", "qlearning", 1.0),
     (True, "reputation", "sarsa", 0.3),            # non-dyadic gain: f64 reputation planes

@@ -197,6 +197,7 @@ class BatchEngine:
         # unchanged, only the order of launches across groups)
         self.cache_bytes = int(float(os.environ.get("SPGG_CACHE_MB", "240")) * 2**20)
         self.chunk = max(1, int(os.environ.get("SPGG_CHUNK", "64")))
+        self.enqueue_chunk = int(os.environ.get("SPGG_ENQ_CHUNK", "8"))
         total = self.state_bytes_per_replica() * self.R
         self.waves = 1 if rng == "inject" else int(max(1, min(self.R, -(-total // self.cache_bytes))))
         if streams is None:
@@ -398,10 +399,13 @@ class BatchEngine:
                 self.t += 1
         else:
             t0, end = self.t, self.t + n_steps
-            if self.resident >= self.G:   # every group resident: one enqueue per group
-                chunks = [(t0, n_steps)]
-            else:                         # cache blocking: groups take turns, chunk iterations each
-                chunks = [(t, min(self.chunk, end - t)) for t in range(t0, end, self.chunk)]
+            # groups are enqueued round-robin, k iterations at a time: with every group
+            # resident this only interleaves the host's launches across the streams (all
+            # of them start within k launches, instead of the last group waiting for the
+            # host to enqueue every other group's n_steps); with cache blocking it is
+            # also the turn length of a wave
+            k = self.chunk if self.resident < self.G else self.enqueue_chunk
+            chunks = [(t, min(k, end - t)) for t in range(t0, end, k)] if k > 0 else [(t0, n_steps)]
             self._enqueue(lambda g, s, c: C.check(self.lib.spgg_step(g["ctx"], c[0], c[1], s), g["ctx"],
                                                   "spgg_step"), rounds=chunks)
             self.t += n_steps

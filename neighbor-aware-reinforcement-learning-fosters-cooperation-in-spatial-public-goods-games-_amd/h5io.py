@@ -3,6 +3,10 @@
 h5py is used when importable.  This image has neither h5py nor an HDF5 library,
 so the fallback writes the same dataset names/dtypes/shapes as a NumPy .npz
 archive at exactly the requested path (readable with numpy.load).
+
+A duplicate dataset name raises ValueError, as h5py does: the reference's run
+fails that way when its three tracked positions coincide (L <= 2,
+spgg.py:137, 620-622), after the state and the earlier datasets are written.
 """
 from __future__ import annotations
 
@@ -30,9 +34,10 @@ class NpzFile:
         return self
 
     def __exit__(self, exc_type, *a):
-        if exc_type is None:
-            with open(self.filename, "wb") as f:
-                np.savez(f, **self.data)
+        # like closing an h5py.File: what was created so far is kept, and an error
+        # raised inside the block (e.g. a duplicate dataset name) propagates
+        with open(self.filename, "wb") as f:
+            np.savez(f, **self.data)
         return False
 
 

@@ -147,8 +147,6 @@ class SPGG:
         finally:
             eng.close()
 
-        write_datasets(filename, hist, snaps, S, R, self.R_min, self.R_max, self.track_positions)
-
         if self.save_png and frames:
             _write_pngs(frames, snapshots_dir)
 
@@ -164,6 +162,10 @@ class SPGG:
             self.algorithm.epsilon = eps_after
             self.epsilon = eps_after
         np.random.set_state((g[0], key, pos, g[3], g[4]))
+
+        # the datasets last: the reference fills its file after the loop, so a write
+        # error (duplicate tracked positions at L <= 2) leaves the state above in place
+        write_datasets(filename, hist, snaps, S, R, self.R_min, self.R_max, self.track_positions)
 
         S_coop = (S == 0).astype(int)
         S_def = (S == 1).astype(int)

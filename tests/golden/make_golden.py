@@ -106,6 +106,32 @@ CASES += [
                                         state_representation="reputation", algorithm="sarsa")),
 ]
 
+# Lattices smaller than the stencils (L < 5: the M=2 offsets wrap onto the same
+# cells several times; L=1: every neighbour is the agent itself, absorbed at t=1).
+CASES += [
+    ("tiny_m1_rep_L1", 41, dict(RUNNER, r=3.0, L=1, iterations=20, influence_factor=1.0,
+                                use_second_order=False, reward_weight_payoff=0.95,
+                                state_representation="reputation")),
+    ("tiny_m2_rep_L2", 42, dict(RUNNER, r=3.6, L=2, iterations=60, influence_factor=1.0,
+                                use_second_order=True, reward_weight_payoff=0.95,
+                                state_representation="reputation")),
+    ("tiny_m2_rep_L3", 43, dict(RUNNER, r=4.0, L=3, iterations=80, influence_factor=1.0,
+                                use_second_order=True, reward_weight_payoff=0.95,
+                                state_representation="reputation")),
+    ("tiny_m1_act_L4", 44, dict(RUNNER, r=3.0, L=4, iterations=80, influence_factor=0.5,
+                                use_second_order=False, reward_weight_payoff=1.0,
+                                state_representation="action")),
+    ("tiny_m2_act_L5", 45, dict(RUNNER, r=3.8, L=5, iterations=80, influence_factor=1.0,
+                                use_second_order=True, reward_weight_payoff=0.95,
+                                state_representation="action")),
+    ("tiny_dq_m2_rep_L3", 46, dict(RUNNER, r=4.0, L=3, iterations=60, influence_factor=1.0,
+                                   use_second_order=True, reward_weight_payoff=0.95,
+                                   state_representation="reputation", algorithm="double_qlearning")),
+    ("tiny_sarsa_m1_rep_L6", 47, dict(RUNNER, r=3.6, L=6, iterations=80, influence_factor=1.0,
+                                      use_second_order=False, reward_weight_payoff=0.95,
+                                      state_representation="reputation", algorithm="sarsa")),
+]
+
 # Cases that need objects (S_in_one, an algorithm instance) are built below.
 SPECIAL = ["sinone_L16", "algo_instance_L16", "absorbing_init_L8",
            "sarsa_instance_L16", "esarsa_instance_L16", "dq_instance_L16"]

@@ -50,10 +50,24 @@ def test_spgg_dropin_matches_reference(name, tmp_path):
     m.save_png = False
     m.folder = str(tmp_path)
     fn = str(tmp_path / "experiment_data.h5")
-    ret = m.run(fn)
-    got = read_datasets(fn)
-    assert set(got) == set(c.datasets), sorted(set(got) ^ set(c.datasets))
-    for k, w in c.datasets.items():
+    L = c.kwargs["L"]
+    tracked = [(L // 2, L // 2), (L // 4, L // 4), (3 * L // 4, 3 * L // 4)]   # spgg.py:137
+    if len(set(tracked)) < 3:
+        # L <= 2: the tracked positions coincide and h5py refuses the second dataset of
+        # the same name (spgg.py:620-622), after the state and the earlier datasets are
+        # written (the fixture's recorder kept every call, so it holds a superset)
+        with pytest.raises(ValueError, match="already exists"):
+            m.run(fn)
+        got = read_datasets(fn)
+        assert "q_c_pos_%d_%d_final" % tracked[0] in got and "Sn_final" not in got
+        want = {k: c.datasets[k] for k in got}
+        ret = None
+    else:
+        ret = m.run(fn)
+        got = read_datasets(fn)
+        want = c.datasets
+    assert set(got) == set(want), sorted(set(got) ^ set(want))
+    for k, w in want.items():
         g = got[k]
         assert g.shape == w.shape, (k, g.shape, w.shape)
         if k in APPROX:
@@ -63,7 +77,8 @@ def test_spgg_dropin_matches_reference(name, tmp_path):
     assert np.array_equal(m.q_table, c.q_table)
     assert np.array_equal(m.R, c.R)
     assert np.array_equal(m._Sn, c.Sn)
-    assert np.array_equal(np.array(ret, dtype=float), c.ret)
+    if ret is not None:
+        assert np.array_equal(np.array(ret, dtype=float), c.ret)
     assert m.algorithm.epsilon == c.epsilon
     if c.tables is not None:   # Double-Q's own tables
         assert np.array_equal(m.algorithm.q_table_1, c.tables[0])

@@ -418,3 +418,35 @@ def test_history_record_stripes_l1000(monkeypatch):
     Q, R, S = eng.final_state(0)
     assert np.array_equal(Q, fin["Q"]) and np.array_equal(S, fin["S"])
     eng.close()
+
+
+def test_max_lattice_size_counts_consistent():
+    """Largest lattice one replica may use (Q < 4 GiB for the kernels' 32-bit offsets:
+    L = 11585, odd, 134 M agents): after two Philox iterations the device-reduced
+    cooperator count of iteration 3's record equals the count of S_3 itself, and
+    the ε schedule is the reference's (size-independent properties; no oracle at
+    this size)."""
+    import ctypes
+    from spgg_amd import _lib as C
+    L = 11585
+    lib = C.load()
+    for bad in (L + 1, 50000):   # past the 32-bit offset range: refused before any allocation
+        cfg = C.Config(device=0, n_rep=1, L=bad, second_order=0, state_mode=C.STATE_REPUTATION,
+                       rng_mode=C.RNG_MODES["philox"], iterations=2, rep_int8=1, algorithm=0)
+        ctx = ctypes.c_void_p()
+        assert lib.spgg_create(ctypes.byref(ctx), cfg) != 0
+    rg = np.random.default_rng(3)   # the reference's init law from a faster generator
+    init = [spgg_amd.engine.InitState(Q=rg.uniform(-0.01, 0.01, size=(L, L, 2, 2)),
+                                      S=rg.integers(0, 2, size=(L, L), dtype=np.int8), tables=None)]
+    eng = BatchEngine(L, 2, [_runner_params(seed=3)], use_second_order=False, rng="philox", init=init)
+    eng.step(2)
+    torch.cuda.synchronize()
+    st = eng.stats_folded().cpu().numpy()[0]
+    S3 = eng.S[0][0] & 1                               # S_3: bit 0 of ping-pong buffer (3 - 1) & 1
+    assert st[1, C.ST_NCOOP] == float((init[0].S == 0).sum())
+    assert st[3, C.ST_NCOOP] == float((S3 == 0).sum().item())
+    assert int(eng.stop_iter[0].item()) == 0
+    h = eng.histories()[0]
+    assert h["epsilon_history_final"][0] == max(0.5 * 0.99, 0.01)
+    assert np.all(np.isfinite(h["neighbor_influence_percent"]))
+    eng.close()

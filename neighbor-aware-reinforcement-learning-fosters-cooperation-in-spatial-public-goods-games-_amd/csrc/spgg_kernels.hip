@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0);
       load_q<QB>(Qr, g, q[u], qb[u]);
       md_own[u] = ld_stream(at(mdr, g));
-      atd_own[u] = ld_stream(at(atdr, g));
+      atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : ld_stream(at(atdr, g));  // 256: atd traffic floor probe
       r += dr;
       c += dc;
       if (c >= tw) {
@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
       const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
                                             act, sn, q[u], qb[u]);
-      if (kappa != 0.0) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
+      if (kappa != 0.0 && !(SPGG_ABLATE & 256)) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
       store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;

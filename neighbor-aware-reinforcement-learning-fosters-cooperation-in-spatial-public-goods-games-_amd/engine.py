@@ -198,6 +198,7 @@ class BatchEngine:
         self.cache_bytes = int(float(os.environ.get("SPGG_CACHE_MB", "240")) * 2**20)
         self.chunk = max(1, int(os.environ.get("SPGG_CHUNK", "64")))
         self.enqueue_chunk = int(os.environ.get("SPGG_ENQ_CHUNK", "8"))
+        self.skip_dead = os.environ.get("SPGG_SKIP_DEAD", "1") != "0"
         total = self.state_bytes_per_replica() * self.R
         self.waves = 1 if rng == "inject" else int(max(1, min(self.R, -(-total // self.cache_bytes))))
         if streams is None:
@@ -322,7 +323,8 @@ class BatchEngine:
             b.eps, b.stats = self.eps[r0].data_ptr(), self.stats[r0].data_ptr()
             b.stop_iter = self.stop_iter[r0].data_ptr()
             C.check(self.lib.spgg_bind(ctx, b), ctx, "spgg_bind")
-            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, bufs=b, stream=streams[g % len(streams)]))
+            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, bufs=b, stream=streams[g % len(streams)],
+                                    live=True))
         self.streams = streams
         self.ctx = self.groups[0]["ctx"]
         tw, th = ctypes.c_int32(), ctypes.c_int32()
@@ -406,13 +408,20 @@ class BatchEngine:
             # also the turn length of a wave
             k = self.chunk if self.resident < self.G else self.enqueue_chunk
             chunks = [(t, min(k, end - t)) for t in range(t0, end, k)] if k > 0 else [(t0, n_steps)]
-            self._enqueue(lambda g, s, c: C.check(self.lib.spgg_step(g["ctx"], c[0], c[1], s), g["ctx"],
-                                                  "spgg_step"), rounds=chunks)
+            self._enqueue(lambda g, s, c: g["live"] and C.check(self.lib.spgg_step(g["ctx"], c[0], c[1], s),
+                                                                g["ctx"], "spgg_step"), rounds=chunks)
             self.t += n_steps
         return n_steps
 
     def all_stopped(self) -> bool:
+        """Host check of the absorbing stops (a sync).  A group whose replicas have all
+        stopped is retired: its later launches would only stage loads and exit (every
+        workgroup of an absorbed replica returns before computing), so they are skipped."""
         self.stopped = self.stop_iter.cpu().numpy().astype(np.int64)
+        if self.skip_dead:
+            for g in self.groups:
+                if g["live"] and np.all(self.stopped[g["r0"]:g["r1"]] != 0):
+                    g["live"] = False
         return bool(np.all(self.stopped != 0))
 
     def flush(self):

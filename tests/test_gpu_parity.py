@@ -450,3 +450,28 @@ def test_max_lattice_size_counts_consistent():
     assert h["epsilon_history_final"][0] == max(0.5 * 0.99, 0.01)
     assert np.all(np.isfinite(h["neighbor_influence_percent"]))
     eng.close()
+
+
+@pytest.mark.parametrize("rng", ["mt19937", "philox"])
+def test_retired_groups_match_full_launches(rng, monkeypatch):
+    """A replica group whose replicas have all absorbed is retired at run()'s host
+    checks (its launches would only exit early): identical results, including the
+    device MT19937 keys and the history records."""
+    L, T = 12, 900
+    reps = ([_runner_params(r=1.0, influence_factor=1.0, seed=60 + s) for s in range(4)] +
+            [_runner_params(r=3.6, influence_factor=1.0, seed=70 + s) for s in range(8)])
+    res = {}
+    for skip in ("0", "1"):
+        monkeypatch.setenv("SPGG_SKIP_DEAD", skip)
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=3)
+        eng.run(chunk=64, snapshots=False)
+        if skip == "1":
+            assert not eng.groups[0]["live"], eng.stopped[:4]   # the r=1.0 group absorbed early
+        res[skip] = ([eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy(),
+                     eng.stop_iter.cpu().numpy(), eng.mt_state.cpu().numpy())
+        eng.close()
+    for a, b in zip(res["0"][0], res["1"][0]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    assert np.array_equal(res["0"][2], res["1"][2]) and np.array_equal(res["0"][3], res["1"][3])
+    np.testing.assert_allclose(res["0"][1], res["1"][1], rtol=0, atol=0)

@@ -217,6 +217,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes per iteration (all replicas), from profiles/r01/current/traffic_*.json",
+                         "traffic_gbs": (traffic / per_step_dev_s / 1e9) if traffic else None,
                          "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
                          "kernel": (f"spgg_step_kernel, {eng.resident} concurrent launches per iteration "
                                     f"(one per replica group/stream)" if args.rng == "philox" else

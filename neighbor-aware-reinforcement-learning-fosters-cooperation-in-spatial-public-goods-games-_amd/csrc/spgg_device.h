@@ -195,16 +195,23 @@ __host__ __device__ inline uint64_t u53_threshold(double thr) {
   return (uint64_t)__builtin_ceil(thr * 9007199254740992.0);
 }
 
-// eps-greedy draw of agent `idx` at iteration t (Philox mode): counter
-// (agent, iteration), key = replica seed mixed with the replica index.
-// u takes 53 bits (w.x>>5, w.y>>6) exactly as numpy's random_sample; the
-// random action is the low bit of w.y, which u does not use.
+// Philox mode: agents 2m and 2m+1 share one Philox2x32-10 block, counter (m, t),
+// key = replica seed mixed with the replica index; the even agent takes w.x, the
+// odd one w.y.  Of an agent's 32 bits, bits 31..1 give u = k / 2^31 (numpy's
+// random_sample has 53 bits: statistical parity only) and bit 0 the random action.
+__device__ __forceinline__ uint2 philox_block(int idx, int t, uint32_t key) {
+  return philox2x32_10(make_uint2((uint32_t)idx >> 1, (uint32_t)t), key);
+}
+// explore = u < eps given thr53 = ceil(eps * 2^53): k * 2^22 < thr53 <=> k / 2^31 < eps
+// (an integer below a ceiling is below the real); rbit = bit 0 (algorithms.py:105-108)
+__device__ __forceinline__ void philox_decide(uint32_t bits, uint64_t thr53, int* explore, int* rbit) {
+  *explore = ((uint64_t)(bits >> 1) << 22) < thr53 ? 1 : 0;
+  *rbit = (int)(bits & 1u);
+}
 __device__ __forceinline__ void philox_draw(int idx, int t, uint32_t key, uint64_t thr53, int* explore,
                                             int* rbit) {
-  const uint2 w = philox2x32_10(make_uint2((uint32_t)idx, (uint32_t)t), key);
-  const uint64_t k = ((uint64_t)(w.x >> 5) << 26) | (w.y >> 6);
-  *explore = k < thr53 ? 1 : 0;                   // algorithms.py:105 (rand < eps)
-  *rbit = (int)(w.y & 1u);                        // algorithms.py:108
+  const uint2 w = philox_block(idx, t, key);
+  philox_decide((idx & 1) ? w.y : w.x, thr53, explore, rbit);
 }
 
 // q[4] accessors with a run-time index e = 2s + a, kept in registers (no scratch).

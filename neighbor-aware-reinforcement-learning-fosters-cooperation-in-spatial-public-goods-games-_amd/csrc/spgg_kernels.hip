@@ -803,12 +803,14 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     for (int u = 0; u < APT; ++u) {
       const int k = tid + u * kBlock;
       const bool own = k < n_own;
-      rc[u] = own ? (r << 16) | (c << 8) : 0;
+      // (TWC tiles: odd lanes shadow the tile's second agent, so lane pairs keep holding
+      // agent pairs (2m, 2m+1) -- the Philox blocks of phase 1b are shared per lane pair)
+      rc[u] = own ? (r << 16) | (c << 8) : (TWC ? (tid & 1) << 8 : 0);
       vbits |= own ? 1u << u : 0u;
       // loads unconditional (threads without a u-th agent read the tile's
       // first one and drop it; md/atd are read even at t = 1, unused there):
       // conditional loads serialise on each other
-      const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0);
+      const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0) + (TWC ? (tid & 1) : 0);
       load_q<QB>(Qr, g, q[u], qb[u]);
       md_own[u] = ld_stream(at(mdr, g));
       atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : ld_stream(at(atdr, g));  // 256: atd traffic floor probe
@@ -1003,6 +1005,24 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   // slot 5 = slot 3 + slot 4 (history means, tolerance 1e-5; slot 5 only feeds
   // the defectors' reward mean as total - over C).
   uint32_t cw0 = 0, cw1 = 0;
+  // Philox bits of the owned slots, one block per lane pair and slot pair: lane pairs
+  // hold agent pairs (2m, 2m+1) in every slot (TWC: even L, x0 and width), so the even
+  // lane computes the blocks of slots j < APT/2, the odd lane those of j + APT/2, and
+  // each hands the partner its half (one DPP swap): half the Philox work per agent
+  constexpr bool PAIRED = RNG == SPGG_RNG_PHILOX && TWC > 0 && APT % 2 == 0 && !(SPGG_ABLATE & 1);
+  uint32_t pbits[APT];
+  if constexpr (PAIRED) {
+    if (acting) {
+      const bool odd = tid & 1;
+#pragma unroll
+      for (int j = 0; j < APT / 2; ++j) {
+        const uint2 w = philox_block((int)agent_of(rc[odd ? j + APT / 2 : j]), t, pkey);
+        const uint32_t keep = odd ? w.y : w.x, recv = partner<1>(odd ? w.x : w.y);
+        pbits[j] = odd ? recv : keep;
+        pbits[j + APT / 2] = odd ? keep : recv;
+      }
+    }
+  }
   {
     double va[8];
 #pragma unroll
@@ -1028,7 +1048,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       if constexpr (AS) so = s_t == 0 ? 1 : 0;
       else so = rep_state_lds<M2>(sRv, ca, ly.aw);
       int ex, rbt;                                          // algorithms.py:105-109
-      draw_pair<RNG>(a, rb, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
+      if constexpr (PAIRED) philox_decide(pbits[u], eps53, &ex, &rbt);
+      else draw_pair<RNG>(a, rb, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
       double qs0, qs1;
       select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
       const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0

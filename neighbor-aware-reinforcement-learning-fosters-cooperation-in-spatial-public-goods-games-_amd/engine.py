@@ -153,6 +153,30 @@ def reference_init(L: int, rs: np.random.RandomState, S_in_one=None, algorithm="
                      mt_pos=int(st[2]), rs=rs)
 
 
+def plan_groups(R: int, L: int, bytes_per_replica: int, cache_bytes: int, streams: Optional[int] = None,
+                single: bool = False):
+    """(waves, groups, resident) for a batch of R replicas of an L x L lattice.
+
+    Replica groups run on concurrent HIP streams: ~1400 workgroups per group kernel
+    (measured best on MI355X for cfg3: 3 groups 78 us/step vs 6 groups 86), at most 8
+    at once; small batches stay in one group (cross-stream ordering costs more than
+    it hides).  A batch whose state exceeds the Infinity-Cache budget is split into
+    `waves` of groups that fit; the `resident` groups of a wave run concurrently and
+    the next wave's groups queue behind them on the same streams.  `streams`
+    overrides the group count; `single` (host-injected draws) forces one group."""
+    if single:
+        return 1, 1, 1
+    waves = int(max(1, min(R, -(-(bytes_per_replica * R) // max(cache_bytes, 1)))))
+    if streams is None:
+        tw = min(L, 40)
+        tiles = -(-L // tw) * -(-L // min(L, 25))
+        per_wave = int(max(1, min(8, round(R / waves * tiles / 1400))))
+        streams = per_wave * waves if waves > 1 else per_wave
+    groups = max(1, min(int(streams), R))
+    resident = groups if waves == 1 else max(1, -(-groups // waves))
+    return waves, groups, resident
+
+
 class BatchEngine:
     """n_rep independent replicas of one (L, M, state) configuration on one device."""
 
@@ -199,12 +223,10 @@ class BatchEngine:
         self.chunk = max(1, int(os.environ.get("SPGG_CHUNK", "64")))
         self.enqueue_chunk = int(os.environ.get("SPGG_ENQ_CHUNK", "8"))
         self.skip_dead = os.environ.get("SPGG_SKIP_DEAD", "1") != "0"
-        total = self.state_bytes_per_replica() * self.R
-        self.waves = 1 if rng == "inject" else int(max(1, min(self.R, -(-total // self.cache_bytes))))
-        if streams is None:
-            streams = int(os.environ.get("SPGG_STREAMS", "0")) or self._auto_streams()
-        self.G = 1 if rng == "inject" else max(1, min(int(streams), self.R))
-        self.resident = self.G if self.waves == 1 else max(1, -(-self.G // self.waves))
+        if streams is None and os.environ.get("SPGG_STREAMS"):
+            streams = int(os.environ["SPGG_STREAMS"]) or None
+        self.waves, self.G, self.resident = plan_groups(
+            self.R, self.L, self.state_bytes_per_replica(), self.cache_bytes, streams, single=rng == "inject")
         self._alloc()
         self._create()
         self.t = 1                 # next iteration to execute
@@ -212,16 +234,6 @@ class BatchEngine:
         self.snapshots = [dict() for _ in range(self.R)]
         self.png_frames = [dict() for _ in range(self.R)]
         self._flushed = False
-
-    def _auto_streams(self):
-        """Replica groups: ~1400 workgroups per group kernel (measured best on MI355X for
-        cfg3: 3 groups 78 us/step vs 6 groups 86), at most 8 concurrent; small batches
-        stay in one group (cross-stream ordering costs more than it hides).  With cache
-        blocking, that many groups per wave."""
-        tw = min(self.L, 40)
-        tiles = -(-self.L // tw) * -(-self.L // min(self.L, 25))
-        per_wave = int(max(1, min(8, round(self.R / self.waves * tiles / 1400))))
-        return per_wave * self.waves if self.waves > 1 else per_wave
 
     def state_bytes_per_replica(self) -> int:
         """Bytes of per-agent state one iteration reads and writes (Q, md, atd, the

@@ -54,7 +54,7 @@ extern "C" {
 /* random stream used by the eps-greedy selects */
 #define SPGG_RNG_INJECT 0   /* caller fills the draw planes per step (host MT19937 etc.) */
 #define SPGG_RNG_MT19937 1  /* device MT19937, bit-identical to numpy.random.RandomState */
-#define SPGG_RNG_PHILOX 2   /* counter-based Philox2x32-10 keyed by (seed, replica), counter (agent, step) */
+#define SPGG_RNG_PHILOX 2   /* counter-based Philox2x32-10 keyed by (seed, replica), counter (agent pair, step) */
 
 /* Per-step history record: stats[rep][stripe][t][SPGG_NSTAT] (float64), t = 0 ..
  * iterations+1, stripe = 0 .. spgg_stat_stripes()-1.  A slot's value is the SUM of its

@@ -155,22 +155,6 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 
 // ---------------------------------------------------------------------------
-// Philox4x32-10 (counter-based): performance-mode eps-greedy draws, keyed by
-// the replica seed, counter (agent, iteration, replica, tag).
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
-  }
-  return c;
-}
-
 // numpy legacy random_sample: 53-bit double from two 32-bit words.
 __device__ __forceinline__ double mt_double(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;

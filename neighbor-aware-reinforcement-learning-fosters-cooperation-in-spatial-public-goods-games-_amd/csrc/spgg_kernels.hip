@@ -506,7 +506,7 @@ __device__ __forceinline__ double expected_q(double v0, double v1, double eps) {
 }
 
 // Draw pair k of agent g at iteration t: explore flag (rand < thr) and the
-// randint bit.  Philox: counter (agent, t + k*2^26) under the replica key;
+// randint bit.  Philox: the agent's half of block (agent pair, t + k*2^26) under the replica key;
 // device MT19937 / inject: planes 2k, 2k+1 of the draw record.
 template <int RNG>
 __device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, int t, uint32_t key, uint64_t thr,

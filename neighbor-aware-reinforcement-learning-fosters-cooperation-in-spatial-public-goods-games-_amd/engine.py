@@ -14,7 +14,8 @@ Random streams:
     and randint(0,2,(L,L)) (algorithms.py:105,108) -- plus SARSA's two
     further selects and Double-Q's table choice -- bit-identically.
   * "inject": the host draws each step (tests / debugging).
-  * "philox": counter-based per-agent stream; statistical parity only.
+  * "philox": counter-based Philox2x32-10 stream (one block per agent pair and
+    iteration); statistical parity only.
 """
 from __future__ import annotations
 

@@ -1585,11 +1585,12 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
 }
 
 // Below this many workgroups per launch (at the operator's agents per thread)
-// a batch runs one agent per thread.  0: never by default -- measured on one
-// L=200 replica the 4x workgroups lose (11.6 vs 10.6 us/step): every workgroup
-// adds its history atomics to the same replica record, 160 per address instead
-// of 40.  The mode stays selectable (SPGG_APT=1) and under test.
-constexpr long long kSmallBatchTiles = 0;
+// a batch runs one agent per thread (4x the workgroups, each a quarter as long).
+// Measured with the striped history record (which keeps the atomics per address
+// at <= 64 per iteration): one L=200 replica (40 tiles) 10.8 -> 10.2 us/step with
+// one agent per thread, 8 replicas (320 tiles, M=2) 16.2 -> 17.0, one L=1000
+// replica (1000 tiles) 28.1 -> 53.9.  SPGG_APT=1 / =<max> forces either.
+constexpr long long kSmallBatchTiles = 128;
 
 // Workgroups per history-record stripe (spgg_stat_stripes).
 constexpr int kTilesPerStripe = 64;

@@ -390,7 +390,16 @@ def test_spgg_dropin_max_agents_per_thread(name, tmp_path, monkeypatch):
 
 
 def test_one_agent_per_thread_mode_selectable(monkeypatch):
-    """SPGG_APT=1: tiles of <= 256 agents (one per thread); default: 1000-agent tiles at L=200."""
+    """Default: one agent per thread (tiles <= 256 agents) for a batch of fewer than 128
+    1000-agent tiles (one L=200 replica), 1000-agent tiles above (8 replicas); SPGG_APT
+    forces either."""
+    eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
+    assert eng.tile[0] * eng.tile[1] <= 256
+    eng.close()
+    eng = BatchEngine(200, 5, [_runner_params(seed=s) for s in range(8)], use_second_order=False, rng="philox")
+    assert eng.tile == (40, 25)
+    eng.close()
+    _force_apt(monkeypatch, "4")
     eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
     assert eng.tile == (40, 25)
     eng.close()

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 8
+#define SPGG_ABI_VERSION 9
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -96,6 +96,11 @@ typedef struct {
   int32_t rep_int8;      /* 1: R buffers hold int8 multiples of each replica's rep_unit
                             (exact when gains/bounds are dyadic multiples, see below) */
   int32_t algorithm;     /* SPGG_ALG_* */
+  int32_t batch_reps;    /* replicas of the whole batch whose buffers this context's
+                            replicas are a slice of (>= n_rep; 0 = n_rep).  The tiling
+                            (agents per thread, tile shape, border-record layout, history
+                            stripes) is chosen from it, so every context of one batch
+                            (replica groups on separate streams) gets the same layout. */
 } spgg_config;
 
 /* Per-replica constants, precomputed by the host in the reference's own
@@ -191,8 +196,12 @@ typedef struct {
 int spgg_abi_version(void);
 /* Number of draw planes one iteration of `algorithm` consumes: 2, 6 (SARSA), 2, 3 (Double-Q). */
 int spgg_draw_planes(int32_t algorithm);
+/* Detail of the context's last failure; with ctx == NULL, of the calling thread's
+ * last failed spgg_create. */
 const char* spgg_last_error(const spgg_ctx* ctx);
 
+/* Environment knob read here: SPGG_APT = "1" (one agent per thread) or "max" (the
+ * operator's maximum) forces the tiling; any other value fails with SPGG_E_ARG. */
 int spgg_create(spgg_ctx** out, const spgg_config* cfg);
 /* Copies n_rep host records to the device (stream-ordered on the null stream). */
 int spgg_set_params(spgg_ctx* ctx, const spgg_rep_params* params);

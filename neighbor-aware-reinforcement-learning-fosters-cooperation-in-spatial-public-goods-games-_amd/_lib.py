@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -40,7 +40,8 @@ class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("n_rep", ctypes.c_int32), ("L", ctypes.c_int32),
                 ("second_order", ctypes.c_int32), ("state_mode", ctypes.c_int32),
                 ("rng_mode", ctypes.c_int32), ("iterations", ctypes.c_int32),
-                ("rep_int8", ctypes.c_int32), ("algorithm", ctypes.c_int32)]
+                ("rep_int8", ctypes.c_int32), ("algorithm", ctypes.c_int32),
+                ("batch_reps", ctypes.c_int32)]
 
 
 class RepParams(ctypes.Structure):
@@ -121,5 +122,5 @@ def load(path: str | None = None):
 def check(rc: int, ctx=None, what: str = "", lib=None):
     if rc != OK:
         lib = lib or load()
-        detail = lib.spgg_last_error(ctx).decode() if ctx else ""
+        detail = (lib.spgg_last_error(ctx) or b"").decode()  # ctx None: last spgg_create failure
         raise SpggError(f"{what} failed (rc={rc}): {detail}")

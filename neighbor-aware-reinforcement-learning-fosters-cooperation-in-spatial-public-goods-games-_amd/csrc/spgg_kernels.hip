@@ -1574,8 +1574,16 @@ int twc_of(const spgg_config& cfg, int TW, int TH) {
   return (TW == 40 && cfg.L % 40 == 0 && cfg.L >= 120 && TH <= 25) ? 40 : 0;
 }
 
+// spgg_last_error(NULL): the calling thread's last spgg_create failure
+thread_local std::string g_create_err;
+
 int fail(spgg_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
+  return code;
+}
+
+int create_fail(int code, const std::string& msg) {
+  g_create_err = msg;
   return code;
 }
 
@@ -1733,38 +1741,56 @@ int spgg_draw_planes(int32_t algorithm) {
   return draw_planes(algorithm);
 }
 
-const char* spgg_last_error(const spgg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* spgg_last_error(const spgg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
 int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
-  if (!out || !cfg) return SPGG_E_ARG;
+  if (!out || !cfg) return create_fail(SPGG_E_ARG, "spgg_create: null argument");
   *out = nullptr;
+  g_create_err.clear();
   if (cfg->n_rep < 1 || cfg->L < 1 || cfg->iterations < 0 || (long long)cfg->L * cfg->L > (1LL << 30))
-    return SPGG_E_ARG;
-  if (cfg->state_mode != SPGG_STATE_REPUTATION && cfg->state_mode != SPGG_STATE_ACTION) return SPGG_E_ARG;
-  if (cfg->rng_mode < SPGG_RNG_INJECT || cfg->rng_mode > SPGG_RNG_PHILOX) return SPGG_E_ARG;
-  if (cfg->algorithm < SPGG_ALG_QLEARNING || cfg->algorithm > SPGG_ALG_DOUBLE_Q) return SPGG_E_ARG;
-  if (cfg->iterations >= (1 << 26)) return SPGG_E_ARG;  // Philox counter: t + pair*2^26
-  if ((long long)cfg->n_rep * cfg->L * cfg->L > (1LL << 31) - 1) return SPGG_E_ARG;
+    return create_fail(SPGG_E_ARG, "spgg_create: n_rep >= 1, 1 <= L <= 32768, iterations >= 0 required");
+  if (cfg->state_mode != SPGG_STATE_REPUTATION && cfg->state_mode != SPGG_STATE_ACTION)
+    return create_fail(SPGG_E_ARG, "spgg_create: unknown state_mode");
+  if (cfg->rng_mode < SPGG_RNG_INJECT || cfg->rng_mode > SPGG_RNG_PHILOX)
+    return create_fail(SPGG_E_ARG, "spgg_create: unknown rng_mode");
+  if (cfg->algorithm < SPGG_ALG_QLEARNING || cfg->algorithm > SPGG_ALG_DOUBLE_Q)
+    return create_fail(SPGG_E_ARG, "spgg_create: unknown algorithm");
+  if (cfg->iterations >= (1 << 26))  // Philox counter: t + pair*2^26
+    return create_fail(SPGG_E_ARG, "spgg_create: iterations >= 2^26");
+  if (cfg->batch_reps != 0 && cfg->batch_reps < cfg->n_rep)
+    return create_fail(SPGG_E_ARG, "spgg_create: batch_reps < n_rep");
+  if ((long long)cfg->n_rep * cfg->L * cfg->L > (1LL << 31) - 1)
+    return create_fail(SPGG_E_ARG, "spgg_create: n_rep * L * L >= 2^31");
   // the step kernel addresses a replica's arrays with 32-bit byte offsets (Q: qw doubles per agent)
-  if ((long long)cfg->L * cfg->L * spgg_impl::qw_of(cfg->algorithm) * 8 > 0xFFFFFFFFLL) return SPGG_E_ARG;
-  spgg_ctx* c = new (std::nothrow) spgg_ctx();
-  if (!c) return SPGG_E_ARG;
-  c->cfg = *cfg;
-  c->n = cfg->L * cfg->L;
+  if ((long long)cfg->L * cfg->L * spgg_impl::qw_of(cfg->algorithm) * 8 > 0xFFFFFFFFLL)
+    return create_fail(SPGG_E_ARG, "spgg_create: a replica's Q table exceeds 4 GiB (32-bit offsets)");
   // Agents per thread: the operator's maximum (tiles of up to 1024 agents), or
   // one for a batch that would launch fewer than kSmallBatchTiles workgroups
-  // (4x the workgroups, each a quarter as long); SPGG_APT=1 / =<max> forces either.
+  // (4x the workgroups, each a quarter as long).  Decided from the WHOLE batch
+  // (batch_reps), so the replica groups of one batch share one tiling: their
+  // border-record and history-record strides must agree.  SPGG_APT = 1 / max forces either.
   const int apt_max = spgg_impl::apt_of(cfg->algorithm);
-  c->apt = apt_max;
+  int apt = apt_max;
   {
     int tw4, th4;
     choose_tile(cfg->L, kBlock * apt_max, &tw4, &th4);
-    const long long tiles4 = (long long)cfg->n_rep * ((cfg->L + tw4 - 1) / tw4) * ((cfg->L + th4 - 1) / th4);
-    const char* e = getenv("SPGG_APT");
-    const int forced = e ? atoi(e) : 0;
-    if (forced == 1 || forced == apt_max) c->apt = forced;
-    else if (tiles4 < kSmallBatchTiles) c->apt = 1;
+    const long long reps = cfg->batch_reps > 0 ? cfg->batch_reps : cfg->n_rep;
+    const long long tiles4 = reps * ((cfg->L + tw4 - 1) / tw4) * ((cfg->L + th4 - 1) / th4);
+    if (const char* e = getenv("SPGG_APT")) {
+      if (!strcmp(e, "max") || atoi(e) == apt_max) apt = apt_max;
+      else if (!strcmp(e, "1")) apt = 1;
+      else
+        return create_fail(SPGG_E_ARG, std::string("SPGG_APT=") + e + ": expected 1 or max (" +
+                                           std::to_string(apt_max) + " agents per thread for this operator)");
+    } else if (tiles4 < kSmallBatchTiles) {
+      apt = 1;
+    }
   }
+  spgg_ctx* c = new (std::nothrow) spgg_ctx();
+  if (!c) return create_fail(SPGG_E_ARG, "spgg_create: out of host memory");
+  c->cfg = *cfg;
+  c->n = cfg->L * cfg->L;
+  c->apt = apt;
   choose_tile(cfg->L, kBlock * c->apt, &c->TW, &c->TH);
   if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;
@@ -1787,7 +1813,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   const int js = spgg_impl::js_of(cfg->second_order != 0), jr = spgg_impl::jr_of();
   if (c->lds_bytes > 160 * 1024 || ly.sw * ly.sh > js * kBlock || ly.aw * ly.ah > jr * kBlock) {
     delete c;
-    return SPGG_E_ARG;
+    return create_fail(SPGG_E_ARG, "spgg_create: tile windows exceed the kernel's LDS / staging budget");
   }
   int rc = hip_check(c, hipSetDevice(cfg->device), "hipSetDevice");
   if (!rc) rc = build_ring_table(c);
@@ -1796,6 +1822,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     if (c->lds_bytes > 160 * 1024) rc = fail(c, SPGG_E_ARG, "tile LDS footprint exceeds 160 KB");
   }
   if (rc) {
+    g_create_err = c->err;
     spgg_destroy(c);
     return rc;
   }

@@ -298,7 +298,7 @@ class BatchEngine:
         cfg = C.Config(device=self.dev.index, n_rep=self.R, L=self.L, second_order=int(self.M2),
                        state_mode=C.STATE_ACTION if self.state_rep == "action" else C.STATE_REPUTATION,
                        rng_mode=C.RNG_MODES[self.rng], iterations=self.T, rep_int8=int(self.rep_int8),
-                       algorithm=self.alg)
+                       algorithm=self.alg, batch_reps=self.R)   # one tiling for every group
         params = [p.to_c() for p in self.reps]
         for k, p in enumerate(params):
             p.stream_id = k
@@ -313,18 +313,22 @@ class BatchEngine:
             cfg.n_rep = r1 - r0
             ctx = ctypes.c_void_p()
             C.check(self.lib.spgg_create(ctypes.byref(ctx), cfg), None, "spgg_create")
+            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, stream=streams[g % len(streams)], live=True))
             arr = (C.RepParams * (r1 - r0))(*params[r0:r1])
             C.check(self.lib.spgg_set_params(ctx, arr), ctx, "spgg_set_params")
-            if g == 0:   # border records and history-record stripes: library-defined sizes
-                per = ctypes.c_int64()
-                C.check(self.lib.spgg_pub_doubles(ctx, ctypes.byref(per)), ctx, "spgg_pub_doubles")
-                self.pub = torch.zeros((2, self.R, max(1, per.value)), dtype=torch.float64, device=self.dev)
-                ns = ctypes.c_int32()
-                C.check(self.lib.spgg_stat_stripes(ctx, ctypes.byref(ns)), ctx, "spgg_stat_stripes")
-                self.stripes = int(ns.value)
+            # border records and history-record stripes: library-defined sizes, which the
+            # shared buffers' per-replica strides assume to be the same for every group
+            layout = self._layout(ctx)
+            if g == 0:
+                self.layout = layout
+                tile, per, self.stripes = layout
+                self.pub = torch.zeros((2, self.R, max(1, per)), dtype=torch.float64, device=self.dev)
                 self.stats = torch.zeros((self.R, self.stripes, self.T + 2, C.NSTAT), dtype=torch.float64,
                                          device=self.dev)
                 self.stats[:, 0, 1, C.ST_NCOOP] = torch.from_numpy(self._ncoop0).to(self.dev)
+            elif layout != self.layout:
+                raise C.SpggError(f"replica group {g} got tiling {layout} != group 0's {self.layout} "
+                                  "(tile, border-record doubles, stripes): shared buffer strides would disagree")
             b = C.Buffers()   # the group's replica slice of every buffer
             for i in range(2):
                 b.S[i], b.R[i] = self.S[i][r0].data_ptr(), self.Rep[i][r0].data_ptr()
@@ -336,13 +340,20 @@ class BatchEngine:
             b.eps, b.stats = self.eps[r0].data_ptr(), self.stats[r0].data_ptr()
             b.stop_iter = self.stop_iter[r0].data_ptr()
             C.check(self.lib.spgg_bind(ctx, b), ctx, "spgg_bind")
-            self.groups.append(dict(r0=r0, r1=r1, ctx=ctx, bufs=b, stream=streams[g % len(streams)],
-                                    live=True))
+            self.groups[-1]["bufs"] = b
         self.streams = streams
         self.ctx = self.groups[0]["ctx"]
+        self.tile = self.layout[0]
+
+    def _layout(self, ctx):
+        """(tile shape, border-record doubles per replica, history stripes) of a context."""
         tw, th = ctypes.c_int32(), ctypes.c_int32()
-        C.check(self.lib.spgg_tile_shape(self.ctx, ctypes.byref(tw), ctypes.byref(th)), self.ctx, "tile")
-        self.tile = (tw.value, th.value)
+        C.check(self.lib.spgg_tile_shape(ctx, ctypes.byref(tw), ctypes.byref(th)), ctx, "spgg_tile_shape")
+        per = ctypes.c_int64()
+        C.check(self.lib.spgg_pub_doubles(ctx, ctypes.byref(per)), ctx, "spgg_pub_doubles")
+        ns = ctypes.c_int32()
+        C.check(self.lib.spgg_stat_stripes(ctx, ctypes.byref(ns)), ctx, "spgg_stat_stripes")
+        return (tw.value, th.value), int(per.value), int(ns.value)
 
     def _enqueue(self, fn, rounds=(None,)):
         """For each round, run fn(group, stream_handle[, round]) on every group's

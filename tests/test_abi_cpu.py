@@ -47,3 +47,32 @@ def test_argument_errors_without_device():
     n = ctypes.c_int32()
     assert lib.spgg_stat_stripes(None, ctypes.byref(n)) == _lib.E_ARG
     assert lib.spgg_destroy(None) == _lib.OK
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_create_failures_report_a_reason(monkeypatch):
+    """spgg_create refuses bad configurations before any device call and says why through
+    spgg_last_error(NULL); an SPGG_APT value other than 1 / max is an error, not ignored."""
+    lib = _lib.load()
+
+    def create(**kw):
+        base = dict(device=0, n_rep=2, L=200, second_order=0, state_mode=_lib.STATE_REPUTATION,
+                    rng_mode=_lib.RNG_PHILOX, iterations=10, rep_int8=1, algorithm=_lib.ALG_QLEARNING)
+        base.update(kw)
+        ctx = ctypes.c_void_p()
+        rc = lib.spgg_create(ctypes.byref(ctx), _lib.Config(**base))
+        assert not ctx.value
+        return rc, lib.spgg_last_error(None).decode()
+
+    rc, msg = create(batch_reps=1)
+    assert rc == _lib.E_ARG and "batch_reps" in msg
+    rc, msg = create(algorithm=9)
+    assert rc == _lib.E_ARG and "algorithm" in msg
+    monkeypatch.setenv("SPGG_APT", "3")
+    rc, msg = create()
+    assert rc == _lib.E_ARG and "SPGG_APT=3" in msg and "max" in msg
+    monkeypatch.setenv("SPGG_APT", "2")   # Double-Q's maximum, not Q-learning's
+    rc, msg = create(algorithm=_lib.ALG_QLEARNING)
+    assert rc == _lib.E_ARG and "4 agents per thread" in msg
+    with pytest.raises(_lib.SpggError, match="SPGG_APT=2"):
+        _lib.check(rc, None, "spgg_create")

@@ -97,8 +97,6 @@ def _oracle_final(L, T, p, seed, M2, state, algorithm="qlearning"):
 
 def _force_apt(monkeypatch, apt, alg="qlearning"):
     """Agents per thread of the step kernel: "1" (small-batch mode) or "max" (4; Double-Q 2)."""
-    if apt == "max":
-        apt = "2" if alg == "double_qlearning" else "4"
     monkeypatch.setenv("SPGG_APT", apt)
 
 
@@ -318,6 +316,28 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
 
 
 @pytest.mark.parametrize("rng", ["philox", "mt19937"])
+def test_groups_straddling_small_batch_threshold_share_one_tiling(rng):
+    """7 x L=200 over 2 streams: groups of 4 (160 1000-agent tiles) and 3 replicas (120,
+    under the 128-tile small-batch threshold on its own).  The tiling is chosen from the
+    whole batch, so both groups use the same tile shape, border-record and history-record
+    strides, and the results equal the one-stream run's bit for bit."""
+    L, T = 200, 30
+    reps = [_runner_params(r=2.5 + 0.4 * s, influence_factor=0.5 * (s % 3), seed=90 + s) for s in range(7)]
+    res = {}
+    for G in (1, 2):
+        eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=G)
+        assert eng.G == G and eng.tile == (40, 25)
+        assert len({eng._layout(g["ctx"]) for g in eng.groups}) == 1
+        eng.run(snapshots=False)
+        res[G] = ([eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy())
+        eng.close()
+    for a, b in zip(res[1][0], res[2][0]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    np.testing.assert_allclose(res[1][1], res[2][1], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("rng", ["philox", "mt19937"])
 def test_cache_blocked_waves_match_concurrent_groups(rng, monkeypatch):
     """Infinity-Cache blocking (groups take turns on shared streams, chunk
     iterations at a time) only reorders launches across independent groups:
@@ -399,7 +419,7 @@ def test_one_agent_per_thread_mode_selectable(monkeypatch):
     eng = BatchEngine(200, 5, [_runner_params(seed=s) for s in range(8)], use_second_order=False, rng="philox")
     assert eng.tile == (40, 25)
     eng.close()
-    _force_apt(monkeypatch, "4")
+    _force_apt(monkeypatch, "max")
     eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
     assert eng.tile == (40, 25)
     eng.close()

@@ -46,10 +46,19 @@ using namespace spgg;
 // Timing-only ablation builds (-DSPGG_ABLATE=mask; results are WRONG):
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
-//   16 = no workgroup totals (final barrier + epilogue), 128 = memory only (the owned loads,
+//   16 = no workgroup totals (final barrier + epilogue), 512 = no per-agent Q / md / atd loads
+//   (synthetic values), 2048 = no per-agent Q / md / atd stores, 128 = memory only (the owned loads,
 //   staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
+#endif
+// Pending-NI record per agent (A/B knob): 0 = max_diff (f64) + |alpha*td'| (f32); 1 = a
+// 32-bit pair of reward codes (the agent's and its best neighbour's payoff inputs, from which
+// the next launch recomputes both rewards, max_diff and the diagnostic |alpha*td'| exactly:
+// 16 B less traffic per agent-step, bit-identical, but measured 3 us/step SLOWER on cfg3 --
+// the two payoff recomputes cost more VALU time than the bytes save; profiles/r02/).
+#ifndef SPGG_PEND_CODES
+#define SPGG_PEND_CODES 0
 #endif
 #ifndef SPGG_PRIO
 #define SPGG_PRIO 0  // wave priority while a workgroup issues its loads (0: off)
@@ -167,7 +176,7 @@ constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_Code, bytes;
 };
 
 // Pitch of the plus-count plane: one 64-lane wave row per region row.
@@ -193,6 +202,7 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_D = off;    off += ((l.sw * l.sh + kPcPitch + 15) / 16) * 16;  // + slack: full-wave row reads
   l.off_A = off;    off += ((na + 15) / 16) * 16;
   l.off_PC = off;   off += (l.ah + 2) * kPcPitch;
+  l.off_Code = off; off += SPGG_PEND_CODES ? ((na * 2 + 15) / 16) * 16 : 0;
   l.bytes = off;
   return l;
 }
@@ -446,20 +456,37 @@ __device__ __forceinline__ void build_plus_counts(uint8_t* pc, const uint8_t* d,
 // group defector counts are plus counts at the cell and its four axial
 // neighbours, each a byte offset into tb = the table of the cell's own
 // strategy indexed by defector count; summed in the reference's group order,
-// normalised.
+// normalised.  *code: the cell's reward code (pay_code).
+#define T_AT(t, o) (*reinterpret_cast<const double*>((t) + (o)))
 __device__ __forceinline__ double payoff_pc(const uint8_t* pc, int ry, int rx, const double* tb, double norm_min,
-                                            double norm_den, double norm_rcp) {
+                                            double norm_den, double norm_rcp, uint32_t* code = nullptr) {
   const uint8_t* p = pc + ry * kPcPitch + rx + 1;  // plus count of N0[i-1, j]
   const char* t = reinterpret_cast<const char*>(tb);
-#define T_AT(o) (*reinterpret_cast<const double*>(t + (o)))
-  double tot = T_AT(p[kPcPitch]);             // group (0,0)  -> N0[i,j]
-  tot = tot + T_AT(p[0]);                      // group (1,0)  -> N0[i-1,j]
-  tot = tot + T_AT(p[2 * kPcPitch]);           // group (-1,0) -> N0[i+1,j]
-  tot = tot + T_AT(p[kPcPitch - 1]);           // group (1,1)  -> N0[i,j-1]
-  tot = tot + T_AT(p[kPcPitch + 1]);           // group (-1,1) -> N0[i,j+1]
-#undef T_AT
+  const uint32_t x0 = p[kPcPitch], x1 = p[0], x2 = p[2 * kPcPitch], x3 = p[kPcPitch - 1], x4 = p[kPcPitch + 1];
+  double tot = T_AT(t, x0);                   // group (0,0)  -> N0[i,j]
+  tot = tot + T_AT(t, x1);                     // group (1,0)  -> N0[i-1,j]
+  tot = tot + T_AT(t, x2);                     // group (-1,0) -> N0[i+1,j]
+  tot = tot + T_AT(t, x3);                     // group (1,1)  -> N0[i,j-1]
+  tot = tot + T_AT(t, x4);                     // group (-1,1) -> N0[i,j+1]
+  if (code) *code = (x0 >> 3) | x1 | (x2 << 3) | (x3 << 6) | (x4 << 9);  // x_k = 8 * defector count
   return div_uniform(tot - norm_min, norm_den, norm_rcp);  // (tot - (r-5)) / (4r - (r-5))
 }
+
+// Reward code of an agent: the five group defector counts (3 bits each, bits 0-14,
+// in the reference's group order) and its strategy (bit 15, 1 = D) -- everything its
+// payoff depends on.  pay_code recomputes the payoff from it with payoff_pc's exact
+// operations (same table entries, same order), hence the same double.
+__device__ __forceinline__ double payoff_code(uint32_t code, const double* tab, double norm_min, double norm_den,
+                                              double norm_rcp) {
+  const char* t = reinterpret_cast<const char*>(tab + ((code >> 15) & 1 ? 6 : 0));
+  double tot = T_AT(t, (code & 7) << 3);
+  tot = tot + T_AT(t, code & 0x38);
+  tot = tot + T_AT(t, (code >> 3) & 0x38);
+  tot = tot + T_AT(t, (code >> 6) & 0x38);
+  tot = tot + T_AT(t, (code >> 9) & 0x38);
+  return div_uniform(tot - norm_min, norm_den, norm_rcp);
+}
+#undef T_AT
 
 // 1/x to full f64 precision for DIAGNOSTIC quotients only (history values,
 // tolerance 1e-5): hardware estimate + two Newton steps, no IEEE division.
@@ -544,11 +571,11 @@ __device__ __forceinline__ int draw_table1(const TileArgs& a, size_t rb, int g, 
 typedef double vd2 __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (SPGG_NT != 0) return __builtin_nontemporal_load(p);
+  if constexpr (SPGG_NT == 1) return __builtin_nontemporal_load(p);
   else return *p;
 }
 template <typename T>
-__device__ __forceinline__ void st_stream(T* p, T v) {
+__device__ __forceinline__ void st_stream(T* p, T v) {  // SPGG_NT=2: stores only
   if constexpr (SPGG_NT != 0) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
@@ -574,6 +601,30 @@ __device__ __forceinline__ void store_q(double* Qr, uint32_t agent, const double
   if constexpr (QB) {
     st_stream(qo + 2, vd2{qb[0], qb[1]});
     st_stream(qo + 3, vd2{qb[2], qb[3]});
+  }
+}
+
+// Stores of the Q entries launch t changed: e_new (TD of t) and e_old (NI term of t-1,
+// -1 if none); every other entry keeps its value in memory.  SPGG_QSTORE: 0 = the whole
+// 32-byte row pair, 1 = the 16-byte rows holding the changed entries, 2 = the 8-byte
+// entries themselves.  Double-Q: whole rows of both tables.
+#ifndef SPGG_QSTORE
+#define SPGG_QSTORE 0
+#endif
+template <int QB>
+__device__ __forceinline__ void store_q_changed(double* Qr, uint32_t agent, const double (&q)[4],
+                                                const double (&qb)[QB ? 4 : 1], int e_new, int e_old) {
+  if constexpr (QB || SPGG_QSTORE == 0) {
+    store_q<QB>(Qr, agent, q, qb);
+  } else if constexpr (SPGG_QSTORE == 1) {
+    vd2* qo = at(reinterpret_cast<vd2*>(Qr), agent * 2);
+    const int rn = e_new >> 1;
+    st_stream(qo + rn, rn ? vd2{q[2], q[3]} : vd2{q[0], q[1]});
+    if (e_old >= 0 && (e_old >> 1) != rn) st_stream(qo + (rn ^ 1), rn ? vd2{q[0], q[1]} : vd2{q[2], q[3]});
+  } else {
+    double* qo = at(Qr, agent * 4);
+    st_stream(qo + e_new, q_get(q, e_new));
+    if (e_old >= 0 && e_old != e_new) st_stream(qo + e_old, q_get(q, e_old));
   }
 }
 
@@ -666,6 +717,23 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
   }
 }
 
+// Diagnostic |diag_alpha*td'| of iteration t-1, recomputed by launch t from the pending
+// record (reward codes): q / qb hold the table after t-1's TD update and before its NI
+// term (the in-place Q between launches), e = (s_old, a), sn = s_t, rew = the agent's
+// reward of t-1 -- td_update's diagnostic operations exactly (spgg.py:446-475).  SARSA's
+// diagnostic needs its own select draw of t-1 (spgg.py:452), so SARSA stores the value.
+template <int ALG, typename PT>
+__device__ __forceinline__ float diag_td_pending(const double (&q)[4], const double (&qb)[ALG == ALG_DQ ? 4 : 1],
+                                                 int e, int sn, double rew, const PT& pg, double eps_prev) {
+  if constexpr (ALG == ALG_DQ) {
+    return diag_td_dq(q, qb, e, sn, rew, pg);
+  } else {
+    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];
+    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps_prev) : fmax(w0, w1);
+    return (float)fabs(pg.diag_alpha * ((rew + pg.diag_gamma * target2) - q_get(q, e)));
+  }
+}
+
 // ONE launch = iteration t of every replica (or, fin_only, the final deferred
 // NI term).  TWC > 0: compile-time tile width, every tile full width (host:
 // L % TWC == 0), so LDS pitches and region divisions are immediates.
@@ -721,6 +789,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   constexpr int QB = ALG == ALG_DQ ? 1 : 0;
   constexpr int QW = QB ? 8 : 4;
   constexpr int PF = spgg_impl::pf_of(ALG);
+  // pending NI record: reward codes (CODES), else max_diff + |alpha*td'|; the
+  // diagnostic is stored (ATD) where it cannot be recomputed from the codes
+  constexpr bool CODES = SPGG_PEND_CODES != 0;
+  constexpr bool ATD = !CODES || ALG == ALG_SARSA;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -751,10 +823,12 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint8_t* sD = smem + ly.off_D;
   uint8_t* sA = smem + ly.off_A;
   uint8_t* sPC = smem + ly.off_PC;
+  uint16_t* sCode = reinterpret_cast<uint16_t*>(smem + ly.off_Code);  // reward codes (CODES)
   // this replica's arrays: scalar bases, 32-bit element offsets (at())
   const size_t rb = (size_t)rep * n;
   double* Qr = a.Q + rb * QW;
   double* mdr = a.md + rb;
+  uint32_t* pendr = reinterpret_cast<uint32_t*>(a.md) + rb;  // CODES: [rep][n] uint32 in the md buffer
   float* atdr = a.atd + rb;
   const uint8_t* Sin = a.S_in + rb;
   uint8_t* Sout = a.S_out + rb;
@@ -790,8 +864,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   unsigned vbits = 0;  // bit u: slot u holds an owned agent
   double q[APT][4];
   double qb[APT][QB ? 4 : 1];
-  double md_own[APT];
-  float atd_own[APT];
+  double md_own[CODES ? 1 : APT];
+  uint32_t pend_own[CODES ? APT : 1];
+  float atd_own[ATD ? APT : 1];
   const int n_own = th * tw;
   const uint32_t g00 = (uint32_t)(y0 * L + x0);
   // (row < 256, L < 2^24: a full-rate 24-bit multiply instead of the quarter-rate 32-bit one)
@@ -811,9 +886,19 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       // first one and drop it; md/atd are read even at t = 1, unused there):
       // conditional loads serialise on each other
       const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0) + (TWC ? (tid & 1) : 0);
-      load_q<QB>(Qr, g, q[u], qb[u]);
-      md_own[u] = ld_stream(at(mdr, g));
-      atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : ld_stream(at(atdr, g));  // 256: atd traffic floor probe
+      if (SPGG_ABLATE & 512) {  // compute-floor probe: no per-agent loads
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[u][k] = (double)((g + k) & 15) * 1e-3;
+        if constexpr (QB) for (int k = 0; k < 4; ++k) qb[u][QB ? k : 0] = q[u][k];
+        if constexpr (CODES) pend_own[u] = g & 0x7fff7fffu;
+        else md_own[u] = 0.0;
+        if constexpr (ATD) atd_own[u] = 0.f;
+      } else {
+        load_q<QB>(Qr, g, q[u], qb[u]);
+        if constexpr (CODES) pend_own[u] = ld_stream(at(pendr, g));
+        else md_own[u] = ld_stream(at(mdr, g));
+        if constexpr (ATD) atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : ld_stream(at(atdr, g));  // 256: atd traffic floor probe
+      }
       r += dr;
       c += dc;
       if (c >= tw) {
@@ -924,8 +1009,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
       store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
-      *at(mdr, agent_of(rc[u])) = md_own[u];
-      *at(atdr, agent_of(rc[u])) = atd_own[u];
+      if constexpr (CODES) *at(pendr, agent_of(rc[u])) = pend_own[u];
+      else *at(mdr, agent_of(rc[u])) = md_own[u];
+      if constexpr (ATD) *at(atdr, agent_of(rc[u])) = atd_own[u];
       *at(Sout, agent_of(rc[u])) = sSv[(r + HS) * ly.sw + (c + HS)];
       if (!AS) *at(Rout, agent_of(rc[u])) = sRv[(r + HA) * ly.aw + (c + HA)];
     }
@@ -941,6 +1027,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     float pct = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.0;
+    // eps of iteration t-1 (Expected SARSA's diagnostic target)
+    const double eps_prev = (CODES && ALG == ALG_ES && pending) ? a.eps[(size_t)rep * a.slots + t - 1] : 0.0;
     if (pending) {
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
@@ -952,7 +1040,26 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         // U(-0.01,0.01) draws and TD sums of finite values give +0 for exact zeros),
         // and the NI percent is exactly 0
         if (kappa != 0.0) {
-          const double nu = pending_nu(b, md_own[u], kappa, lam_den, lam_rcp);
+          double mdp;
+          float atdv;
+          if constexpr (CODES) {
+            // both rewards of t-1 from their codes (phase 1b's operations: w_P*P + w_rep*rr),
+            // the best neighbour's action from the match bit; max(0, max_diff) as phase 2
+            const uint32_t pc2 = pend_own[u];
+            const int act = b & 1, an = ((b >> 2) & 1) ? act : act ^ 1;
+            const double rs = w_p * payoff_code(pc2 & 0xffffu, tab, hp.norm_min, hp.norm_den, hp.norm_rcp) +
+                              w_rep * (act == 0 ? 0.5 : 0.0);
+            const double rn = w_p * payoff_code(pc2 >> 16, tab, hp.norm_min, hp.norm_den, hp.norm_rcp) +
+                              w_rep * (an == 0 ? 0.5 : 0.0);
+            const double md = rn - rs;
+            mdp = md > 0.0 ? md : 0.0;
+            if constexpr (ATD) atdv = atd_own[u];
+            else atdv = diag_td_pending<ALG>(q[u], qb[u], e, (b >> 4) & 1, rs, hp, eps_prev);
+          } else {
+            mdp = md_own[u];
+            atdv = atd_own[u];
+          }
+          const double nu = pending_nu(b, mdp, kappa, lam_den, lam_rcp);
           // Q[s,a] += nu as exact masked FMAs: fma(1, nu, x) = x + nu, fma(0, nu, x) = x
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -963,7 +1070,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
           // NI percent (spgg.py:512; x100 applied to the workgroup total), in f32:
           // a history mean (tolerance 1e-5), each term a ratio in [0, 1]
           const float anu = fabsf((float)nu);
-          pct = __builtin_fmaf(anu * __builtin_amdgcn_rcpf((atd_own[u] + anu) + 1e-8f), (float)vmu, pct);
+          pct = __builtin_fmaf(anu * __builtin_amdgcn_rcpf((atdv + anu) + 1e-8f), (float)vmu, pct);
         }
         const double cm = ((b >> 3) & 1) ? 0.0 : vmu;                  // prev_S of t-1 == C
 #pragma unroll
@@ -1036,8 +1143,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int cs = (r + HS) * ly.sw + (c + HS);
       const int ca = (r + HA) * ly.aw + (c + HA);
       const int s_t = sSv[cs] & 1;
+      uint32_t code;
       const double P = payoff_pc(sPC, r + HA, c + HA, tab + (s_t ? 6 : 0), hp.norm_min, hp.norm_den,
-                                 hp.norm_rcp);
+                                 hp.norm_rcp, &code);
+      if (CODES && acting) sCode[ca] = (uint16_t)(code | (s_t << 15));
       const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sRv[ca];
       const double cmask = s_t ? 0.0 : vmu;
       va[0] = __builtin_fma(P, vmu, va[0]);                 // spgg.py:388-390
@@ -1108,7 +1217,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
           }
         }
       }
-      const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp);
+      uint32_t code;
+      const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp,
+                                 &code);
       const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sRv[ay * ly.aw + ax]);
       int ex, rbt;
       draw_pair<RNG>(a, rb, g, t, pkey, eps53, 0, &ex, &rbt);
@@ -1120,6 +1231,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       sA[ca] = (uint8_t)act;
       sRn[ca] = (RT)rn;
       sRew[ca] = wpp + wrr;
+      if constexpr (CODES) sCode[ca] = (uint16_t)(code | ((b & 1u) << 15));
     }
   }
   __syncthreads();
@@ -1141,10 +1253,15 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, kappa != 0.0, rew, so,
-                                            act, sn, q[u], qb[u]);
-      if (kappa != 0.0 && !(SPGG_ABLATE & 256)) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
-      store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
+      // (the diagnostic only where it is stored; with reward codes the next launch recomputes it)
+      const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, ATD && kappa != 0.0,
+                                            rew, so, act, sn, q[u], qb[u]);
+      if (ATD && kappa != 0.0 && !(SPGG_ABLATE & (256 | 2048))) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
+      if (!(SPGG_ABLATE & 2048)) {
+        // entry the NI term of t-1 changed in phase 1a (none at t = 1 or with kappa == 0)
+        const int e_old = (pending && kappa != 0.0) ? pending_entry(sSv[(r + HS) * ly.sw + (c + HS)]) : -1;
+        store_q_changed<QB>(Qr, agent_of(rc[u]), q[u], qb[u], so * 2 + act, e_old);
+      }
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -1153,18 +1270,25 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                           ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
       double md = sRew[nb[0]] - rew;
       int abest = sA[nb[0]], ks = 0;  // best neighbour's action (and offset index, M=2)
+      int cbest = nb[0];              // best neighbour's region cell (its reward code)
 #pragma unroll
       for (int kk = 1; kk < KN; ++kk) {
         const double d = sRew[nb[kk]] - rew;
         const bool better = d > md;
         md = better ? d : md;
         abest = better ? (int)sA[nb[kk]] : abest;
+        if constexpr (CODES) cbest = better ? nb[kk] : cbest;
         if constexpr (M2) ks = better ? kk : ks;
       }
       const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = fmax(bmax, mdp);
-      st_stream(at(mdr, agent_of(rc[u])), mdp);
+      if (SPGG_ABLATE & 2048) {
+      } else if constexpr (CODES) {
+        st_stream(at(pendr, agent_of(rc[u])), (uint32_t)sCode[ca] | ((uint32_t)sCode[cbest] << 16));
+      } else {
+        st_stream(at(mdr, agent_of(rc[u])), mdp);
+      }
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
       if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring

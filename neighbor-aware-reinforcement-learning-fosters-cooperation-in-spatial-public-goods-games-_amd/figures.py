@@ -5,10 +5,11 @@ Restates the reference's plot consumers -- `src/visualization/plotting.py:1-362`
 `plot_state_comparison`), `scripts/plot_figures.py:19-126` (which experiment
 folder feeds which figure) and `scripts/plot_state_comparison.py:19-80` -- over
 the per-experiment `data/experiment_data.h5` files that `SPGG.run` and the
-batched sweep (`sweep.py`) write.  Those files are HDF5 when h5py is importable
-and otherwise an .npz archive under the same name with the same datasets
-(`h5io.py`); `load_data` reads either, so the figures regenerate from this
-build's output whichever writer produced it.
+batched sweep (`sweep.py`) write.  Those files are HDF5 (h5py, or the HDF5 C
+library through `h5native` when h5py is absent) or, without any HDF5 library, an
+.npz archive under the same name with the same datasets (`h5io.py`); `load_data`
+reads each, so the figures regenerate from this build's output whichever writer
+produced it.
 
 Same function names, arguments, dataset names, axes, limits and file names as
 the reference; missing files or datasets print a warning and leave the curve
@@ -31,13 +32,12 @@ if not os.environ.get("DISPLAY"):
     matplotlib.use("Agg")
 import matplotlib.pyplot as plt  # noqa: E402
 
-from .h5io import h5py  # noqa: E402  (None in this image)
+from .h5io import read_dataset  # noqa: E402
 
 DATA_FILE = os.path.join("data", "experiment_data.h5")
 FIGURES = ("2", "4", "6", "7", "8", "9")
 KAPPAS_FIG2 = (0.0, 0.5, 1.0, 1.5, 2.0)          # plot_figures.py:61-63
 R_SNAPSHOT_TIMES = (100, 1000, 10000)             # plotting.py:197
-_HDF5_MAGIC = b"\x89HDF\r\n\x1a\n"
 
 
 def setup_matplotlib_for_publication(font_size_pt=12):
@@ -59,15 +59,8 @@ def setup_matplotlib_for_publication(font_size_pt=12):
 
 
 def _read_one(filepath: str, name: str) -> Optional[np.ndarray]:
-    with open(filepath, "rb") as fh:
-        head = fh.read(8)
-    if head == _HDF5_MAGIC:
-        if h5py is None:
-            raise OSError("HDF5 file but h5py is not importable")
-        with h5py.File(filepath, "r") as f:
-            return f[name][:] if name in f else None
-    with np.load(filepath, allow_pickle=False) as z:  # h5io.NpzFile output
-        return z[name] if name in z.files else None
+    # HDF5 (h5py, or the HDF5 C library when h5py is absent) or h5io's .npz sink
+    return read_dataset(filepath, name)
 
 
 def load_data(filepath, dataset_name):

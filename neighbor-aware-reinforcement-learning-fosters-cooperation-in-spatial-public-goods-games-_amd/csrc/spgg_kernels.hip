@@ -1268,15 +1268,25 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int nb[12] = {ca - w, ca + w, ca - 1, ca + 1,
                           ca - 2 * w, ca + 2 * w, ca - 2, ca + 2,
                           ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
-      double md = sRew[nb[0]] - rew;
-      int abest = sA[nb[0]], ks = 0;  // best neighbour's action (and offset index, M=2)
+      // every neighbour's reward and action read up front (unconditional LDS loads, in
+      // flight together): a select of a load inside the scan was compiled into a load under
+      // an exec mask per neighbour, each waiting for the one before
+      double rw[KN];
+      int an[KN];
+#pragma unroll
+      for (int kk = 0; kk < KN; ++kk) {
+        rw[kk] = sRew[nb[kk]];
+        an[kk] = sA[nb[kk]];
+      }
+      double md = rw[0] - rew;
+      int abest = an[0], ks = 0;      // best neighbour's action (and offset index, M=2)
       int cbest = nb[0];              // best neighbour's region cell (its reward code)
 #pragma unroll
       for (int kk = 1; kk < KN; ++kk) {
-        const double d = sRew[nb[kk]] - rew;
+        const double d = rw[kk] - rew;
         const bool better = d > md;
         md = better ? d : md;
-        abest = better ? (int)sA[nb[kk]] : abest;
+        abest = better ? an[kk] : abest;
         if constexpr (CODES) cbest = better ? nb[kk] : cbest;
         if constexpr (M2) ks = better ? kk : ks;
       }
@@ -1302,7 +1312,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         rec[(PF - 1) * a.PB] = mdp;
       }
       // group composition on S_{t+1}, spgg.py:585-592: nibble nd of gcn
-      const int nd = act + sA[ca - w] + sA[ca + w] + sA[ca - 1] + sA[ca + 1];
+      const int nd = act + an[0] + an[1] + an[2] + an[3];   // (the four axial neighbours, loaded above)
       gcn += one << (4 * nd);
       if (md > 0.0) {                                       // spgg.py:520-523
         cw1 += one << 16;

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 9
+#define SPGG_ABI_VERSION 10
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -58,19 +58,21 @@ extern "C" {
 
 /* Per-step history record: stats[rep][stripe][t][SPGG_NSTAT] (float64), t = 0 ..
  * iterations+1, stripe = 0 .. spgg_stat_stripes()-1.  A slot's value is the SUM of its
- * stripes, except SPGG_ST_GMAX: the MAX.  Integer counts are stored exactly as float64. */
+ * stripes, except SPGG_ST_GMAX: the MAX.  Integer counts are stored exactly as float64.
+ * The slots marked (derived) are filled by spgg_history_finalize from the counted ones
+ * (slot 0 holds the group composition of S_1, written by iteration 1's prologue). */
 enum {
   SPGG_ST_NCOOP = 0,      /* #S_t==0 at iteration start (spgg.py:383)            */
-  SPGG_ST_SUMP = 1,       /* sum P                       (spgg.py:388)            */
-  SPGG_ST_SUMP_C = 2,     /* sum P over S_t==0           (spgg.py:389)            */
-  SPGG_ST_SUMP_D = 3,     /* sum P over S_t==1           (spgg.py:390)            */
+  SPGG_ST_SUMP = 1,       /* sum P (derived)             (spgg.py:388)            */
+  SPGG_ST_SUMP_C = 2,     /* sum P over S_t==0 (derived) (spgg.py:389)            */
+  SPGG_ST_SUMP_D = 3,     /* sum P over S_t==1 (derived) (spgg.py:390)            */
   SPGG_ST_SUMR = 4,       /* sum R_t                     (spgg.py:394)            */
   SPGG_ST_SW_CD = 5,      /* switches C->D               (spgg.py:419)            */
   SPGG_ST_SW_DC = 6,      /* switches D->C               (spgg.py:420)            */
-  SPGG_ST_SUM_WPP = 7,    /* sum w_P*P                   (spgg.py:425)            */
-  SPGG_ST_SUM_WRR = 8,    /* sum w_rep*rep_reward        (spgg.py:426)            */
+  SPGG_ST_SUM_WPP = 7,    /* sum w_P*P (derived)         (spgg.py:425)            */
+  SPGG_ST_SUM_WRR = 8,    /* sum w_rep*rep_reward (derived) (spgg.py:426)         */
   SPGG_ST_SUM_REW_C = 9,  /* sum reward over a==0        (spgg.py:542)            */
-  SPGG_ST_SUM_REW_D = 10, /* sum reward over a==1        (spgg.py:543)            */
+  SPGG_ST_SUM_REW_D = 10, /* sum reward over a==1 (derived) (spgg.py:543)         */
   SPGG_ST_SUM_RATIO_C = 11, /* sum rep-reward ratio over a==0 (spgg.py:533-535)   */
   SPGG_ST_GC0 = 12,       /* 12..17: #agents with d defectors in 5-pt group (spgg.py:586-592) */
   SPGG_ST_NMD_POS = 18,   /* #agents with max_diff > 0   (spgg.py:521)            */
@@ -216,6 +218,13 @@ int spgg_step(spgg_ctx* ctx, int32_t t0, int32_t n_steps, void* hip_stream);
 /* Apply the deferred neighbor-influence term of iteration t_last (the last
  * executed one) and its Q statistics.  Call once after the final spgg_step. */
 int spgg_flush(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
+
+/* Fill the derived history slots (SPGG_ST_SUMP / _SUMP_C / _SUMP_D of iterations 1..last,
+ * SPGG_ST_SUM_WPP / _SUM_WRR / _SUM_REW_D of the executed steps; last = a replica's
+ * absorbing iteration, else t_last) from the counted ones.  Idempotent; enqueue it after
+ * the steps whose records are read.  Replaces: the per-step np.mean calls of
+ * spgg.py:383-394, 529-545 for those values. */
+int spgg_history_finalize(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
 
 /* Draw the RNG bytes of one iteration only (MT19937 mode; for tests). */
 int spgg_draw(spgg_ctx* ctx, int32_t t, void* hip_stream);

@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -33,7 +33,8 @@ NSTAT = 34
 
 EXPORTED = ("spgg_abi_version", "spgg_last_error", "spgg_create", "spgg_set_params",
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
-            "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes")
+            "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
+            "spgg_history_finalize")
 
 
 class Config(ctypes.Structure):
@@ -98,6 +99,8 @@ def load(path: str | None = None):
         lib.spgg_step.argtypes = [vp, i32, i32, vp]
         lib.spgg_flush.restype = ctypes.c_int
         lib.spgg_flush.argtypes = [vp, i32, vp]
+        lib.spgg_history_finalize.restype = ctypes.c_int
+        lib.spgg_history_finalize.argtypes = [vp, i32, vp]
         lib.spgg_draw.restype = ctypes.c_int
         lib.spgg_draw.argtypes = [vp, i32, vp]
         lib.spgg_payoff.restype = ctypes.c_int

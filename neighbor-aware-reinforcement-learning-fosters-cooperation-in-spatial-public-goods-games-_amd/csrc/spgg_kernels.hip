@@ -1021,7 +1021,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (!fin_only) build_plus_counts(sPC, sDv, ly.sw, ah + 2);
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
-  // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C, 8 NI percent
+  // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C; the NI percent
+  // (pct_t1) is reduced with phase 1b's values
+  float pct_t1 = 0.f;
   {
     double v[8];
     float pct = 0.f;
@@ -1082,8 +1084,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
     }
     wave_partials<8>(v, red, 0);
-    double pv[1] = {(double)pct};
-    wave_partials<1>(pv, red, 8);
+    pct_t1 = pct;  // reduced with phase 1b's values
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
@@ -1105,12 +1106,13 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   __syncthreads();  // plus counts and ring records complete
 
   // ---- phase 1b: iteration start + action select for owned agents --------
-  // f64 value slots (-> slot t): 0 sumP, 1 sumP over C, 2 sumR, 3 sum w_P*P,
-  // 4 sum w_rep*rr, 5 sum reward, 6 sum reward over C, 7 sum ratio over C.
-  // Slots 4 and 5 are not accumulated: w_rep*rr is w_rep*0.5 for every
-  // cooperating action and 0 otherwise, so slot 4 = (C actions) * w_rep*0.5 and
-  // slot 5 = slot 3 + slot 4 (history means, tolerance 1e-5; slot 5 only feeds
-  // the defectors' reward mean as total - over C).
+  // f64 value slots: 0 sum R (slot t), 1 sum reward over C actions (slot t), 2 sum
+  // reputation-reward ratio over C actions (slot t), 3 NI percent (slot t-1, phase 1a).
+  // The payoff sums (sum P, over C / D, sum w_P*P), sum w_rep*rr and the reward sum
+  // over D are NOT accumulated per agent: spgg_history_finalize derives them from the
+  // group-composition and cooperator counts (a group with d defectors pays its members
+  // (5-d)*pay_c + d*pay_d in total, so sum P over the lattice is a 6-bin histogram dot
+  // a table; history means, tolerance 1e-5).
   uint32_t cw0 = 0, cw1 = 0;
   // Philox bits of the owned slots, one block per lane pair and slot pair: lane pairs
   // hold agent pairs (2m, 2m+1) in every slot (TWC: even L, x0 and width), so the even
@@ -1131,9 +1133,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
   }
   {
-    double va[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) va[k] = 0.0;
+    double va[4] = {0.0, 0.0, 0.0, 0.0};
+    RVal<RQ> rsum = 0;  // sum R_t (int8 units: an exact integer sum)
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       if (fin_only) continue;
@@ -1148,10 +1149,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                                  hp.norm_rcp, &code);
       if (CODES && acting) sCode[ca] = (uint16_t)(code | (s_t << 15));
       const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sRv[ca];
-      const double cmask = s_t ? 0.0 : vmu;
-      va[0] = __builtin_fma(P, vmu, va[0]);                 // spgg.py:388-390
-      va[1] = __builtin_fma(P, cmask, va[1]);
-      va[2] = __builtin_fma((double)r_t, vmu, va[2]);       // spgg.py:394 (units if RQ)
+      if constexpr (RQ) rsum += one ? r_t : 0;             // spgg.py:394 (units)
+      else rsum = __builtin_fma(r_t, vmu, rsum);
       if (!acting) continue;
       int so;                                               // spgg.py:409
       if constexpr (AS) so = s_t == 0 ? 1 : 0;
@@ -1174,16 +1173,15 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
       cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
       cw1 += act == 0 ? one : 0u;
-      va[3] = __builtin_fma(wpp, vmu, va[3]);               // spgg.py:425-426
       const double am = act ? 0.0 : vmu;
-      va[6] = __builtin_fma(rew, am, va[6]);
+      va[1] = __builtin_fma(rew, am, va[1]);                // spgg.py:542
       // reputation-reward ratio (x100 applied to the total): exactly 0 when w_rep == 0
-      if (w_rep != 0.0) va[7] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[7]);
+      if (w_rep != 0.0) va[2] = __builtin_fma(fabs(wrr) * rcp_diag(fabs(rew) + 1e-9), am, va[2]);
     }
-    va[4] = (double)(cw1 & 0xffffu) * (w_rep * 0.5);      // spgg.py:425-426
-    va[5] = va[3] + va[4];                                  // spgg.py:529-545
-    // red[wave*64 + 16..23]: va[0..7] (reduced here: frees their registers for phases 1c / 2)
-    if (!(SPGG_ABLATE & 8)) wave_partials<8>(va, red, 16);
+    va[0] = (double)rsum;
+    va[3] = (double)pct_t1;
+    // red[wave*64 + 16..19]: va[0..3] (reduced here: frees their registers for phases 1c / 2)
+    if (!(SPGG_ABLATE & 8)) wave_partials<4>(va, red, 16);
   }
   STAMP(3);
 
@@ -1354,27 +1352,21 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         slot = t - 1;
         if (tid < 4) { k = SPGG_ST_SUMQ + tid; src = tid; }
         else if (tid < 8) { k = SPGG_ST_SUMQ_C + tid - 4; src = tid; }
-        else if (tid == 8) { k = SPGG_ST_SUM_PCT; src = 8; }
+        else if (tid == 8) { k = SPGG_ST_SUM_PCT; src = 16 + 3; }
         else { k = SPGG_ST_SUMQ_D + tid - 9; src = tid - 9; src_c = tid - 5; }
       }
-    } else if (tid >= 16 && tid < 16 + 22 && !fin_only) {
-      const int j = tid - 16;  // 0-7 va, 8-18 counters, 19-20 derived
-      // record index of value j, one byte each in three 64-bit immediates (a
+    } else if (tid >= 16 && tid < 16 + 14 && !fin_only) {
+      const int j = tid - 16;  // 0-2 va, 3-13 counters
+      // record index of value j, one byte each in two 64-bit immediates (a
       // constant-memory table would cost the epilogue a memory round trip)
-      constexpr uint64_t km0 = stat_bytes(SPGG_ST_SUMP, SPGG_ST_SUMP_C, SPGG_ST_SUMR, SPGG_ST_SUM_WPP,
-                                          SPGG_ST_SUM_WRR, -1 /* reward total: only feeds REW_D */,
-                                          SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C);
-      constexpr uint64_t km1 = stat_bytes(SPGG_ST_SW_CD, SPGG_ST_SW_DC, SPGG_ST_NCOOP, SPGG_ST_NMD_POS,
-                                          SPGG_ST_NMD_POS2, SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2);
-      constexpr uint64_t km2 = stat_bytes(SPGG_ST_GC0 + 3, SPGG_ST_GC0 + 4, SPGG_ST_GC0 + 5, SPGG_ST_SUMP_D,
-                                          SPGG_ST_SUM_REW_D, -1, -1, -1);
-      const uint64_t km = j < 8 ? km0 : (j < 16 ? km1 : km2);
-      k = (int)(int8_t)(uint8_t)(km >> (8 * (j & 7)));
+      constexpr uint64_t km0 = stat_bytes(SPGG_ST_SUMR, SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C, SPGG_ST_SW_CD,
+                                          SPGG_ST_SW_DC, SPGG_ST_NCOOP, SPGG_ST_NMD_POS, SPGG_ST_NMD_POS2);
+      constexpr uint64_t km1 = stat_bytes(SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2, SPGG_ST_GC0 + 3,
+                                          SPGG_ST_GC0 + 4, SPGG_ST_GC0 + 5, -1, -1);
+      k = (int)(int8_t)(uint8_t)((j < 8 ? km0 : km1) >> (8 * (j & 7)));
       src = 16 + j;
-      if (j == 19) { src = 16 + 0; src_c = 16 + 1; }   // sumP over D = sumP - sumP over C
-      if (j == 20) { src = 16 + 5; src_c = 16 + 6; }   // reward over D = total - over C
-      const bool start_val = (j <= 2 || j == 19);      // recorded on the absorbing iteration too
-      if (k >= 0 && (acting || start_val)) slot = (j == 10) ? t + 1 : t;
+      const bool start_val = j == 0;                   // recorded on the absorbing iteration too
+      if (acting || start_val) slot = (j == 5) ? t + 1 : t;
     }
     if (tid == 40 && acting) {  // lattice-wide max |diff| (spgg.py:488)
       double bm = 0.0;
@@ -1387,15 +1379,15 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
     if (slot >= 0) {
       const int j = tid - 16;
-      const bool counter = j >= 8 && j <= 18;
-      const int word = 24 + ((j - 8) >> 1);
+      const bool counter = j >= 3 && j <= 13;
+      const int word = 24 + ((j - 3) >> 1);
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) {
         tot[0] += red[w * 64 + (counter ? word : src)];
         if (src_c >= 0) tot[1] += red[w * 64 + src_c];
       }
       double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
-      if (counter) val = (double)(((unsigned long long)tot[0] >> (16 * ((j - 8) & 1))) & 0xffffu);
+      if (counter) val = (double)(((unsigned long long)tot[0] >> (16 * ((j - 3) & 1))) & 0xffffu);
       // (from LDS: a global read here would wait for every store of the tile)
       if (RQ && k == SPGG_ST_SUMR) val *= hp.rep_unit;
       if (k == SPGG_ST_SUM_PCT || k == SPGG_ST_SUM_RATIO_C) val *= 100.0;  // percent sums
@@ -1417,11 +1409,27 @@ __global__ __launch_bounds__(kBlock) void spgg_publish_init_kernel(TileArgs a) {
   constexpr int PF = spgg_impl::pf_of(ALG);
   const int rep = blockIdx.y;
   const int g = blockIdx.x * kBlock + threadIdx.x;
-  if (g >= a.n) return;
   const int L = a.L;
   const int y = g / L, x = g - (g / L) * L;
   const size_t rb = (size_t)rep * a.n;
-  uint8_t* S = a.S_out;  // S_1, updated in place
+  uint8_t* S = a.S_out;  // S_1, updated in place (bit 4; bit 0 is only read)
+  // group composition of S_1 (defectors in each agent's 5-cell plus, spgg.py:585-592
+  // restated on S_1) -> history slot 0, from which spgg_history_finalize derives
+  // iteration 1's payoff sums (later iterations: the step kernel's counts)
+  __shared__ int gc1[6];
+  if (threadIdx.x < 6) gc1[threadIdx.x] = 0;
+  __syncthreads();
+  if (g < a.n) {
+    const uint8_t* s = S + rb;
+    const int d = (s[g] & 1) + (s[wrap(y - 1, L) * L + x] & 1) + (s[wrap(y + 1, L) * L + x] & 1) +
+                  (s[y * L + wrap(x - 1, L)] & 1) + (s[y * L + wrap(x + 1, L)] & 1);
+    atomicAdd(&gc1[d], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < 6 && gc1[threadIdx.x] != 0)
+    atomicAdd(&a.stats[(size_t)rep * a.stripes * a.slots * SPGG_NSTAT + SPGG_ST_GC0 + threadIdx.x],
+              (double)gc1[threadIdx.x]);
+  if (g >= a.n) return;
   int s1;
   if constexpr (AS) {
     s1 = (S[rb + g] & 1) ? 0 : 1;
@@ -1655,6 +1663,57 @@ __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
   }
   if (tid < 624) gstate[tid] = mt[tid];
   if (tid == 0) gstate[624] = (uint32_t)pos;
+}
+
+// History values derived from device counts (spgg_history_finalize), for iterations
+// t = 1 .. last of each replica (last = its absorbing iteration, else t_last), into
+// stripe 0 (the step kernel adds nothing to these slots):
+//   start of t (spgg.py:383-394): SUMP, SUMP_C, SUMP_D from the group composition of S_t
+//     (slot t-1; slot 0 = S_1, written by the prologue): a group centred on a cell with d
+//     defectors pays its 5-d cooperators pay_c[5-d] and its d defectors pay_d[5-d], so
+//     sum Praw = sum_d GC_d ((5-d) pay_c + d pay_d), over C: sum_d GC_d (5-d) pay_c, and
+//     sum P = (sum Praw - n (r-5)) / (4r - (r-5)) (spgg.py:373-378);
+//   step t (executed steps only, spgg.py:425-426, 529-545): SUM_WPP = w_P sum P,
+//     SUM_WRR = (C actions = NCOOP of slot t+1) * w_rep * 0.5, SUM_REW_D = SUM_WPP + SUM_WRR
+//     - SUM_REW_C.
+// History means: the regrouped sums differ from per-agent accumulation in rounding only.
+__global__ __launch_bounds__(kBlock) void spgg_history_finalize_kernel(double* stats, const int* stop_iter,
+                                                                       const spgg_rep_params* params, int n,
+                                                                       int slots, int stripes, int t_last) {
+  const int rep = blockIdx.y;
+  const int t = blockIdx.x * kBlock + threadIdx.x + 1;
+  const int st = stop_iter[rep];
+  const int last = st ? st : t_last, m = st ? st - 1 : t_last;
+  if (t > last || t + 1 >= slots) return;
+  const size_t stripe_len = (size_t)slots * SPGG_NSTAT;
+  const double* rec = stats + (size_t)rep * stripes * stripe_len;
+  auto total = [&](int slot, int k) {
+    double v = 0.0;
+    for (int sp = 0; sp < stripes; ++sp) v += rec[sp * stripe_len + (size_t)slot * SPGG_NSTAT + k];
+    return v;
+  };
+  const spgg_rep_params& p = params[rep];
+  double praw = 0.0, praw_c = 0.0;
+#pragma unroll
+  for (int d = 0; d <= 5; ++d) {
+    const double gc = total(t - 1, SPGG_ST_GC0 + d);
+    praw_c += gc * ((5 - d) * p.pay_c[5 - d]);
+    praw += gc * ((5 - d) * p.pay_c[5 - d] + d * p.pay_d[5 - d]);
+  }
+  const double nc = total(t, SPGG_ST_NCOOP);
+  const double sump = (praw - n * p.norm_min) / p.norm_den;
+  const double sump_c = (praw_c - nc * p.norm_min) / p.norm_den;
+  double* out = stats + (size_t)rep * stripes * stripe_len + (size_t)t * SPGG_NSTAT;
+  out[SPGG_ST_SUMP] = sump;
+  out[SPGG_ST_SUMP_C] = sump_c;
+  out[SPGG_ST_SUMP_D] = sump - sump_c;
+  if (t <= m) {
+    const double wpp = p.w_p * sump;
+    const double wrr = total(t + 1, SPGG_ST_NCOOP) * (p.w_rep * 0.5);
+    out[SPGG_ST_SUM_WPP] = wpp;
+    out[SPGG_ST_SUM_WRR] = wrr;
+    out[SPGG_ST_SUM_REW_D] = (wpp + wrr) - total(t, SPGG_ST_SUM_REW_C);
+  }
 }
 
 // P of every agent from S_t (epilogue: SPGG.P / run()'s mean(P), spgg.py:378, 637).
@@ -2020,6 +2079,17 @@ int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {
   if (t_last < 1 || t_last > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_flush: bad t_last");
   launch_step(c, t_last + 1, 1, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_flush launch");
+}
+
+int spgg_history_finalize(spgg_ctx* c, int32_t t_last, void* stream) {
+  if (!c) return SPGG_E_ARG;
+  if (!c->bound || !c->params_set) return fail(c, SPGG_E_STATE, "spgg_history_finalize before bind/set_params");
+  if (t_last < 0 || t_last > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_history_finalize: bad t_last");
+  const int slots = c->cfg.iterations + 2;
+  const dim3 grid((slots + kBlock - 1) / kBlock, c->cfg.n_rep);
+  hipLaunchKernelGGL(spgg_history_finalize_kernel, grid, dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
+                     c->buf.stats, c->buf.stop_iter, c->d_params, c->n, slots, c->stripes, t_last);
+  return hip_check(c, hipGetLastError(), "spgg_history_finalize launch");
 }
 
 int spgg_draw(spgg_ctx* c, int32_t t, void* stream) {

@@ -540,8 +540,17 @@ class BatchEngine:
             self.lib.spgg_payoff(g["ctx"], int(t), self.P_buf[g["r0"]].data_ptr(), s), g["ctx"], "spgg_payoff"))
         return self.P_buf.cpu().numpy().reshape(self.R, self.L, self.L)
 
+    def finalize_history(self):
+        """Derived history slots (payoff sums, w_P*P, w_rep*rr, reward over D) of every
+        executed iteration from the counted ones (spgg_history_finalize; idempotent)."""
+        tl = self.t - 1
+        if tl >= 1:
+            self._enqueue(lambda g, s: C.check(self.lib.spgg_history_finalize(g["ctx"], tl, s), g["ctx"],
+                                               "spgg_history_finalize"))
+
     def stats_folded(self):
         """(R, T+2, NSTAT) device tensor of the history record: stripes summed, GMAX maxed."""
+        self.finalize_history()
         st = self.stats.sum(dim=1)
         if self.stripes > 1:
             st[..., C.ST_GMAX] = self.stats[..., C.ST_GMAX].amax(dim=1)

@@ -68,7 +68,7 @@ enum {
   SPGG_ST_SUMP_D = 3,     /* sum P over S_t==1 (derived) (spgg.py:390)            */
   SPGG_ST_SUMR = 4,       /* sum R_t                     (spgg.py:394)            */
   SPGG_ST_SW_CD = 5,      /* switches C->D               (spgg.py:419)            */
-  SPGG_ST_SW_DC = 6,      /* switches D->C               (spgg.py:420)            */
+  SPGG_ST_SW_DC = 6,      /* switches D->C (derived)     (spgg.py:420)            */
   SPGG_ST_SUM_WPP = 7,    /* sum w_P*P (derived)         (spgg.py:425)            */
   SPGG_ST_SUM_WRR = 8,    /* sum w_rep*rep_reward (derived) (spgg.py:426)         */
   SPGG_ST_SUM_REW_C = 9,  /* sum reward over a==0        (spgg.py:542)            */
@@ -220,7 +220,7 @@ int spgg_step(spgg_ctx* ctx, int32_t t0, int32_t n_steps, void* hip_stream);
 int spgg_flush(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
 
 /* Fill the derived history slots (SPGG_ST_SUMP / _SUMP_C / _SUMP_D of iterations 1..last,
- * SPGG_ST_SUM_WPP / _SUM_WRR / _SUM_REW_D of the executed steps; last = a replica's
+ * SPGG_ST_SUM_WPP / _SUM_WRR / _SUM_REW_D / _SW_DC of the executed steps; last = a replica's
  * absorbing iteration, else t_last) from the counted ones.  Idempotent; enqueue it after
  * the steps whose records are read.  Replaces: the per-step np.mean calls of
  * spgg.py:383-394, 529-545 for those values. */

@@ -187,9 +187,12 @@ __device__ __forceinline__ uint2 philox_block(int idx, int t, uint32_t key) {
   return philox2x32_10(make_uint2((uint32_t)idx >> 1, (uint32_t)t), key);
 }
 // explore = u < eps given thr53 = ceil(eps * 2^53): k * 2^22 < thr53 <=> k / 2^31 < eps
-// (an integer below a ceiling is below the real); rbit = bit 0 (algorithms.py:105-108)
+// (an integer below a ceiling is below the real), and for the integer k < 2^31 that is
+// k < ceil(thr53 / 2^22) <= 2^31: one 32-bit compare against a workgroup-uniform bound;
+// rbit = bit 0 (algorithms.py:105-108)
 __device__ __forceinline__ void philox_decide(uint32_t bits, uint64_t thr53, int* explore, int* rbit) {
-  *explore = ((uint64_t)(bits >> 1) << 22) < thr53 ? 1 : 0;
+  const uint32_t thr31 = (uint32_t)((thr53 + ((1ull << 22) - 1)) >> 22);
+  *explore = (bits >> 1) < thr31 ? 1 : 0;
   *rbit = (int)(bits & 1u);
 }
 __device__ __forceinline__ void philox_draw(int idx, int t, uint32_t key, uint64_t thr53, int* explore,

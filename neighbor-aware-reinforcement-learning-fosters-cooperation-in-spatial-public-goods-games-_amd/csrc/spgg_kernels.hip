@@ -144,6 +144,15 @@ __host__ __device__ inline int border_slot(int r, int c, int th, int tw, int HA)
   const int cc = c < HA ? c : c - tw + 2 * HA;
   return 2 * HA * tw + (r - HA) * 2 * HA + cc;
 }
+// The same slot, or -1 for an interior cell, without branches (one per agent in the
+// step kernel's store phase: divergent branches there cost more than the arithmetic).
+__device__ __forceinline__ int border_slot_or_none(int r, int c, int th, int tw, int HA) {
+  const bool top = r < HA, bot = r >= th - HA;
+  const bool left = c < HA, right = c >= tw - HA;
+  const int band = (top ? r : r - th + 2 * HA) * tw + c;
+  const int side = 2 * HA * tw + (r - HA) * 2 * HA + (left ? c : c - tw + 2 * HA);
+  return (top || bot) ? band : ((left || right) ? side : -1);
+}
 
 // Ring cell k of a th x tw tile in region coordinates (ay, ax) of the
 // (th + 2HA) x (tw + 2HA) window: the HA rows above, the HA rows below, then
@@ -1170,8 +1179,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       sRew[ca] = rew;  // (R_{t+1} is stored in phase 2: a store here would make the ring's
                        // record loads wait for it)
       rc[u] |= act | (so << 1) | (s_t << 3);
-      cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419-420
-      cw0 += (s_t == 1 && act == 0) ? one << 16 : 0u;
+      cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419 (D->C: finalize)
       cw1 += act == 0 ? one : 0u;
       const double am = act ? 0.0 : vmu;
       va[1] = __builtin_fma(rew, am, va[1]);                // spgg.py:542
@@ -1299,8 +1307,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
-      if (spgg_impl::is_border(r, c, th, tw, HA)) {  // row s_{t+1} + max_diff for the neighbours' ring
-        double* rec = pout + spgg_impl::border_slot(r, c, th, tw, HA);
+      const int bslot = spgg_impl::border_slot_or_none(r, c, th, tw, HA);
+      if (bslot >= 0) {  // row s_{t+1} + max_diff for the neighbours' ring
+        double* rec = pout + bslot;
         rec[0] = sn ? q[u][2] : q[u][0];
         rec[a.PB] = sn ? q[u][3] : q[u][1];
         if constexpr (QB) {
@@ -1673,9 +1682,9 @@ __global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
 //     defectors pays its 5-d cooperators pay_c[5-d] and its d defectors pay_d[5-d], so
 //     sum Praw = sum_d GC_d ((5-d) pay_c + d pay_d), over C: sum_d GC_d (5-d) pay_c, and
 //     sum P = (sum Praw - n (r-5)) / (4r - (r-5)) (spgg.py:373-378);
-//   step t (executed steps only, spgg.py:425-426, 529-545): SUM_WPP = w_P sum P,
+//   step t (executed steps only, spgg.py:419-420, 425-426, 529-545): SUM_WPP = w_P sum P,
 //     SUM_WRR = (C actions = NCOOP of slot t+1) * w_rep * 0.5, SUM_REW_D = SUM_WPP + SUM_WRR
-//     - SUM_REW_C.
+//     - SUM_REW_C, SW_DC = SW_CD + NCOOP(t+1) - NCOOP(t) (cooperators gained = D->C - C->D).
 // History means: the regrouped sums differ from per-agent accumulation in rounding only.
 __global__ __launch_bounds__(kBlock) void spgg_history_finalize_kernel(double* stats, const int* stop_iter,
                                                                        const spgg_rep_params* params, int n,
@@ -1708,11 +1717,13 @@ __global__ __launch_bounds__(kBlock) void spgg_history_finalize_kernel(double* s
   out[SPGG_ST_SUMP_C] = sump_c;
   out[SPGG_ST_SUMP_D] = sump - sump_c;
   if (t <= m) {
+    const double nc1 = total(t + 1, SPGG_ST_NCOOP);
     const double wpp = p.w_p * sump;
-    const double wrr = total(t + 1, SPGG_ST_NCOOP) * (p.w_rep * 0.5);
+    const double wrr = nc1 * (p.w_rep * 0.5);
     out[SPGG_ST_SUM_WPP] = wpp;
     out[SPGG_ST_SUM_WRR] = wrr;
     out[SPGG_ST_SUM_REW_D] = (wpp + wrr) - total(t, SPGG_ST_SUM_REW_C);
+    out[SPGG_ST_SW_DC] = total(t, SPGG_ST_SW_CD) + nc1 - nc;   // exact integers
   }
 }
 

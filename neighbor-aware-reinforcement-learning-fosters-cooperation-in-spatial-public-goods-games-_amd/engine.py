@@ -158,20 +158,27 @@ def plan_groups(R: int, L: int, bytes_per_replica: int, cache_bytes: int, stream
                 single: bool = False):
     """(waves, groups, resident) for a batch of R replicas of an L x L lattice.
 
-    Replica groups run on concurrent HIP streams: ~1400 workgroups per group kernel
-    (measured best on MI355X for cfg3: 3 groups 78 us/step vs 6 groups 86), at most 8
-    at once; small batches stay in one group (cross-stream ordering costs more than
-    it hides).  A batch whose state exceeds the Infinity-Cache budget is split into
-    `waves` of groups that fit; the `resident` groups of a wave run concurrently and
-    the next wave's groups queue behind them on the same streams.  `streams`
-    overrides the group count; `single` (host-injected draws) forces one group."""
+    Replica groups run on concurrent HIP streams, so one group's launch tail overlaps
+    another's start.  Groups per wave by the wave's 1000-agent tiles (measured on
+    MI355X, profiles/r02/streams_by_batch.txt): >= 2400 tiles 2 groups (105 x L=200:
+    2 groups 64.8 us/step, 3 66.5, 4 75.5; 70 replicas 46.0 / 47.0; cache-blocked 210
+    and 420 replicas 131.9 / 256.5 us at 2 per wave vs 136.8 / 265.3 at 3), 1200-2400
+    tiles 3 groups (35 replicas 27.4 vs 28.2 at 2, 52 replicas 36.2 vs 37.8), fewer
+    tiles one group (cross-stream ordering costs more than it hides); never 4 at once
+    (more streams than the 4 hardware queues serialise).  A batch whose state
+    exceeds the Infinity-Cache budget is split into `waves` of groups that fit; the
+    `resident` groups of a wave run concurrently and the next wave's groups queue
+    behind them on the same streams.  `streams` overrides the group count; `single`
+    (host-injected draws) forces one group."""
     if single:
         return 1, 1, 1
     waves = int(max(1, min(R, -(-(bytes_per_replica * R) // max(cache_bytes, 1)))))
     if streams is None:
         tw = min(L, 40)
         tiles = -(-L // tw) * -(-L // min(L, 25))
-        per_wave = int(max(1, min(8, round(R / waves * tiles / 1400))))
+        tpw = R / waves * tiles
+        per_wave = 2 if tpw >= 2400 else (3 if tpw >= 1200 else 1)
+        per_wave = int(max(1, min(per_wave, -(-R // waves))))
         streams = per_wave * waves if waves > 1 else per_wave
     groups = max(1, min(int(streams), R))
     resident = groups if waves == 1 else max(1, -(-groups // waves))

@@ -13,15 +13,17 @@ def per_rep(L, qw=4, rsz=1):  # engine.state_bytes_per_replica for Q-learning, i
 
 
 @pytest.mark.parametrize("R,L,want", [
-    (105, 200, (1, 3, 3)),     # cfg3: fits the cache, 3 groups of ~1400 workgroups
+    (105, 200, (1, 2, 2)),     # cfg3: fits the cache, 2 groups of 2100 workgroups
+    (52, 200, (1, 3, 3)),      # 2080 tiles: 3 groups
+    (35, 200, (1, 3, 3)),
     (1, 200, (1, 1, 1)),       # cfg2
     (8, 200, (1, 1, 1)),       # cfg4-sized batch: one group
     (126, 200, (2, 4, 2)),     # past the cache: 2 waves of 2 resident groups
-    (210, 200, (2, 6, 3)),
-    (420, 200, (4, 12, 3)),    # 4 waves of cfg3-sized work
+    (210, 200, (2, 4, 2)),
+    (420, 200, (4, 8, 2)),     # 4 waves of cfg3-sized work
     (1, 1000, (1, 1, 1)),      # cfg5
-    (8, 1000, (2, 6, 3)),
-    (3000, 50, (2, 8, 4)),     # many small lattices
+    (8, 1000, (2, 4, 2)),
+    (3000, 50, (2, 4, 2)),     # many small lattices
 ])
 def test_auto_plan(R, L, want):
     assert plan_groups(R, L, per_rep(L), BUDGET) == want

@@ -199,7 +199,7 @@ def main():
     achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
 
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "r01", "current", f"traffic_{args.config}.json")
+    tfile = os.path.join(ROOT, "profiles", "r02", "current", f"traffic_{args.config}.json")
     if os.path.exists(tfile) and args.rng == "philox":
         # measured HBM bytes per agent-step (rocprofv3 PMC passes of this same command)
         traffic = json.load(open(tfile))["bytes_per_agent_step"] * step_agents
@@ -216,7 +216,7 @@ def main():
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_unit": "bytes per iteration (all replicas), from profiles/r01/current/traffic_*.json",
+                         "traffic_unit": "bytes per iteration (all replicas), from profiles/r02/current/traffic_*.json",
                          "traffic_gbs": (traffic / per_step_dev_s / 1e9) if traffic else None,
                          "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
                          "kernel": (f"spgg_step_kernel, {eng.resident} concurrent launches per iteration "

@@ -461,6 +461,30 @@ __device__ __forceinline__ void build_plus_counts(uint8_t* pc, const uint8_t* d,
   }
 }
 
+// The same plane for compile-time-width tiles, four cells per lane: the defector plane
+// (window column j at physical column j + soff, soff <= 1, rows dword-aligned) is read
+// as aligned dwords and the five neighbour bytes of four consecutive cells are funnel
+// shifts of two of them (v_alignbit).  Each byte sum is <= 5 and x8 <= 40, so no byte
+// carries into the next; bytes past the window (uninitialised) feed only higher, unused
+// bytes.  DWPR = dwords per plane row (>= the region width + 2, / 4).
+template <int DWPR>
+__device__ __forceinline__ void build_plus_counts_dw(uint8_t* pc, const uint8_t* dplane, int sw, int rows,
+                                                     int soff) {
+  const uint32_t s0 = 8u * soff, s1 = s0 + 8u, s2 = s0 + 16u;
+  const int swd = sw >> 2;
+  for (int task = threadIdx.x; task < rows * DWPR; task += kBlock) {
+    const int y = task / DWPR, xd = task - (task / DWPR) * DWPR;
+    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(dplane) + y * swd + xd;
+    const uint32_t a0 = r0[0], a1 = r0[1];                    // row y    (the cell above)
+    const uint32_t b0 = r0[swd], b1 = r0[swd + 1];            // row y+1  (left, centre, right)
+    const uint32_t c0 = r0[2 * swd], c1 = r0[2 * swd + 1];    // row y+2  (the cell below)
+    const uint32_t cnt = __builtin_amdgcn_alignbit(a1, a0, s1) + __builtin_amdgcn_alignbit(b1, b0, s0) +
+                         __builtin_amdgcn_alignbit(b1, b0, s1) + __builtin_amdgcn_alignbit(b1, b0, s2) +
+                         __builtin_amdgcn_alignbit(c1, c0, s1);
+    *reinterpret_cast<uint32_t*>(pc + y * kPcPitch + xd * 4) = cnt << 3;
+  }
+}
+
 // Payoff of the region cell (ry, rx) (spgg.py:230-259, 373-377): the five
 // group defector counts are plus counts at the cell and its four axial
 // neighbours, each a byte offset into tb = the table of the cell's own
@@ -1027,7 +1051,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     return;
   }
   // plus counts for the payoffs of phases 1b / 1c (their barrier: after phase 1a)
-  if (!fin_only) build_plus_counts(sPC, sDv, ly.sw, ah + 2);
+  if (!fin_only) {
+    if constexpr (TWC > 0) build_plus_counts_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPC, sD, ly.sw, ah + 2, soffS);
+    else build_plus_counts(sPC, sDv, ly.sw, ah + 2);
+  }
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
   // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C; the NI percent

@@ -132,6 +132,27 @@ __device__ __forceinline__ double block_reduce(double (&v)[K], double* lds) {
   return tot;
 }
 
+// Workgroup-uniform values computed on the VALU (f64 has no scalar ALU) moved back
+// to SGPRs: held in VGPRs they cost every lane two registers for the whole kernel.
+__device__ __forceinline__ double uniform_f64(double x) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(x)));
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32 |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
+// max of two non-NaN doubles as ONE v_max_f64.  fmax() in IEEE mode first quiets
+// each operand that is not provably canonical (v_max_f64 x, x, x), three f64 ops in
+// all; no value here is ever a NaN, and quieting changes no other value (f64
+// denormals are preserved), so the result is the same double.
+__device__ __forceinline__ double max_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Max over the wave, in every lane: permlane32/16 swaps, then DPP partners
 // l^8, l^7, l^2, l^1 (together they span the 16-lane row), no LDS.
 template <int MASK>
@@ -141,16 +162,16 @@ __device__ __forceinline__ double swap_max(double x) {
                             : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
   const auto h = MASK == 32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
                             : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  return fmax(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+  return max_f64(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
 }
 
 __device__ __forceinline__ double wave_max(double v) {
   v = swap_max<32>(v);
   v = swap_max<16>(v);
-  v = fmax(v, partner<8>(v));
-  v = fmax(v, partner<4>(v));
-  v = fmax(v, partner<2>(v));
-  v = fmax(v, partner<1>(v));
+  v = max_f64(v, partner<8>(v));
+  v = max_f64(v, partner<4>(v));
+  v = max_f64(v, partner<2>(v));
+  v = max_f64(v, partner<1>(v));
   return v;
 }
 

@@ -95,7 +95,8 @@ struct TileArgs {
   double* stats;          // [rep][stripe][slot][NSTAT]: a workgroup adds to stripe tile % stripes
   int* stop_iter;
   const spgg_rep_params* params;
-  const int2* ring;       // [tiles_per_rep][ring_max]: {agent index, border-record offset}
+  const int2* ring;       // [tiles_per_rep][ring_max]: {agent index, border-record offset}, then the
+                          // border-slot table: [4 tile shapes][kBlock] x 4 int16 (border_slot_table)
   int L, n, TW, TH, tiles_x, tiles_per_rep, n_rep, slots;
   int PB;                 // border-record slots per tile (pub_slots)
   int ring_max;
@@ -144,9 +145,9 @@ __host__ __device__ inline int border_slot(int r, int c, int th, int tw, int HA)
   const int cc = c < HA ? c : c - tw + 2 * HA;
   return 2 * HA * tw + (r - HA) * 2 * HA + cc;
 }
-// The same slot, or -1 for an interior cell, without branches (one per agent in the
-// step kernel's store phase: divergent branches there cost more than the arithmetic).
-__device__ __forceinline__ int border_slot_or_none(int r, int c, int th, int tw, int HA) {
+// The same slot, or -1 for an interior cell, without branches (the host tabulates it per
+// tile shape and thread for the step kernel's store phase: border_slot_table).
+__host__ __device__ inline int border_slot_or_none(int r, int c, int th, int tw, int HA) {
   const bool top = r < HA, bot = r >= th - HA;
   const bool left = c < HA, right = c >= tw - HA;
   const int band = (top ? r : r - th + 2 * HA) * tw + c;
@@ -671,8 +672,12 @@ __device__ __forceinline__ void select_row(const double (&q)[4], const double (&
     *v0 = s ? m10 : m00;
     *v1 = s ? m11 : m01;
   } else {
-    *v0 = s ? q[2] : q[0];
-    *v1 = s ? q[3] : q[1];
+    // the rows as opaque values: a select of two entries of q would otherwise be folded
+    // into one load at a computed index of q, which keeps q in scratch memory
+    double q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    asm("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+    *v0 = s ? q2 : q0;
+    *v1 = s ? q3 : q1;
   }
 }
 
@@ -684,7 +689,7 @@ __device__ __forceinline__ float diag_td_dq(const double (&q)[4], const double (
   const double m00 = mean2(q[0], qb[0]), m01 = mean2(q[1], qb[1]);
   const double m10 = mean2(q[2], qb[2]), m11 = mean2(q[3], qb[3]);
   const double m0 = sn ? m10 : m00, m1 = sn ? m11 : m01;
-  const double td2 = (rew + pg.diag_gamma * fmax(m0, m1)) - mean2(q_get(q, e), q_get(qb, e));
+  const double td2 = (rew + pg.diag_gamma * max_f64(m0, m1)) - mean2(q_get(q, e), q_get(qb, e));
   return (float)fabs(pg.diag_alpha * td2);
 }
 
@@ -724,7 +729,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     const double qc = act ? o1 : o0;
     double target;
     if constexpr (ALG == ALG_Q) {
-      target = fmax(v0, v1);                                         // algorithms.py:124-127
+      target = max_f64(v0, v1);                                      // algorithms.py:124-127
     } else if constexpr (ALG == ALG_SARSA) {
       int ex, rbt;                                                   // next action, spgg.py:434
       draw_pair<RNG>(a, rb, g, t, key, eps53, 1, &ex, &rbt);
@@ -734,8 +739,13 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     }
     const double td = (rew + gamma * target) - qc;
     const double q1 = qc + alpha * td;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = e == k ? q1 : q[k];
+    // entry (so, act) <- q1: lane masks of so and act combined on the scalar unit (four
+    // v_cmp of e against 0..3 would each take a VALU issue slot)
+    const bool s1 = so != 0, a1 = act != 0;
+    q[0] = (!s1 && !a1) ? q1 : q[0];
+    q[1] = (!s1 && a1) ? q1 : q[1];
+    q[2] = (s1 && !a1) ? q1 : q[2];
+    q[3] = (s1 && a1) ? q1 : q[3];
     if (!diag) return 0.f;
     const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];       // updated table, row s'
     double target2;
@@ -744,7 +754,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
       draw_pair<RNG>(a, rb, g, t, key, eps53, 2, &ex, &rbt);
       target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
     } else {
-      target2 = ALG == ALG_ES ? expected_q(w0, w1, eps) : fmax(w0, w1);
+      target2 = ALG == ALG_ES ? expected_q(w0, w1, eps) : max_f64(w0, w1);
     }
     return (float)fabs(pg.diag_alpha * ((rew + dgamma * target2) - q1));  // Q'[s,a] = q1
   }
@@ -762,7 +772,7 @@ __device__ __forceinline__ float diag_td_pending(const double (&q)[4], const dou
     return diag_td_dq(q, qb, e, sn, rew, pg);
   } else {
     const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];
-    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps_prev) : fmax(w0, w1);
+    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps_prev) : max_f64(w0, w1);
     return (float)fabs(pg.diag_alpha * ((rew + pg.diag_gamma * target2) - q_get(q, e)));
   }
 }
@@ -1002,10 +1012,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (pending)
     for (int k = 0; k < a.stripes; ++k)
       gmax_prev = fmax(gmax_prev, rrow[k * stripe_len + (size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX]);
-  const double lam_den = pending ? gmax_prev + pg.lambda_eps : 1.0;
-  const double lam_rcp = 1.0 / lam_den;  // IEEE, once per workgroup
+  const double lam_den = uniform_f64(pending ? gmax_prev + pg.lambda_eps : 1.0);
+  const double lam_rcp = uniform_f64(1.0 / lam_den);  // IEEE, once per workgroup
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
-  const uint64_t eps53 = u53_threshold(eps_t);  // rand < eps_t as an integer compare
+  const uint64_t eps53 = uniform_u64(u53_threshold(eps_t));  // rand < eps_t as an integer compare
   // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
   const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
                         (uint32_t)pg.stream_id * 0xC2B2AE35u;
@@ -1067,12 +1077,18 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     for (int k = 0; k < 8; ++k) v[k] = 0.0;
     // eps of iteration t-1 (Expected SARSA's diagnostic target)
     const double eps_prev = (CODES && ALG == ALG_ES && pending) ? a.eps[(size_t)rep * a.slots + t - 1] : 0.0;
+    uint8_t sb[APT];  // S_t bytes of the owned agents: s_t (bit 0) and the state (bit 4) go to rc
+#pragma unroll
+    for (int u = 0; u < APT; ++u) {
+      const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
+      sb[u] = sSv[(r + HS) * ly.sw + (c + HS)];
+      rc[u] |= (AS ? 0 : ((sb[u] >> 4) & 1) << 1) | ((sb[u] & 1) << 3);
+    }
     if (pending) {
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
         const double vmu = (vbits >> u) & 1 ? 1.0 : 0.0;
-        const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
-        const uint8_t b = sSv[(r + HS) * ly.sw + (c + HS)];
+        const uint8_t b = sb[u];
         const int e = pending_entry(b);
         // kappa == 0 (a replica-uniform skip): nu = +0, q + 0 == q (Q never holds -0.0:
         // U(-0.01,0.01) draws and TD sums of finite values give +0 for exact zeros),
@@ -1154,20 +1170,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   // hold agent pairs (2m, 2m+1) in every slot (TWC: even L, x0 and width), so the even
   // lane computes the blocks of slots j < APT/2, the odd lane those of j + APT/2, and
   // each hands the partner its half (one DPP swap): half the Philox work per agent
+  // (the blocks of slots 2j and 2j+1 are made just before slot 2j: two bit words live, not APT)
   constexpr bool PAIRED = RNG == SPGG_RNG_PHILOX && TWC > 0 && APT % 2 == 0 && !(SPGG_ABLATE & 1);
   uint32_t pbits[APT];
-  if constexpr (PAIRED) {
-    if (acting) {
-      const bool odd = tid & 1;
-#pragma unroll
-      for (int j = 0; j < APT / 2; ++j) {
-        const uint2 w = philox_block((int)agent_of(rc[odd ? j + APT / 2 : j]), t, pkey);
-        const uint32_t keep = odd ? w.y : w.x, recv = partner<1>(odd ? w.x : w.y);
-        pbits[j] = odd ? recv : keep;
-        pbits[j + APT / 2] = odd ? keep : recv;
-      }
-    }
-  }
   {
     double va[4] = {0.0, 0.0, 0.0, 0.0};
     RVal<RQ> rsum = 0;  // sum R_t (int8 units: an exact integer sum)
@@ -1179,7 +1184,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const double vmu = one ? 1.0 : 0.0;
       const int cs = (r + HS) * ly.sw + (c + HS);
       const int ca = (r + HA) * ly.aw + (c + HA);
-      const int s_t = sSv[cs] & 1;
+      const int s_t = (rc[u] >> 3) & 1;                     // (S_t bits, recorded in phase 1a)
       uint32_t code;
       const double P = payoff_pc(sPC, r + HA, c + HA, tab + (s_t ? 6 : 0), hp.norm_min, hp.norm_den,
                                  hp.norm_rcp, &code);
@@ -1188,9 +1193,19 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       if constexpr (RQ) rsum += one ? r_t : 0;             // spgg.py:394 (units)
       else rsum = __builtin_fma(r_t, vmu, rsum);
       if (!acting) continue;
+      if constexpr (PAIRED) {
+        if (u % 2 == 0) {  // even lane: block of slot u, odd lane: slot u+1; swap halves
+          const bool odd = tid & 1;
+          const uint2 w = philox_block((int)agent_of(rc[odd ? u + 1 : u]), t, pkey);
+          const uint32_t keep = odd ? w.y : w.x, recv = partner<1>(odd ? w.x : w.y);
+          pbits[u] = odd ? recv : keep;
+          pbits[u + 1] = odd ? keep : recv;
+        }
+      }
       int so;                                               // spgg.py:409
       if constexpr (AS) so = s_t == 0 ? 1 : 0;
-      else so = rep_state_lds<M2>(sRv, ca, ly.aw);
+      else so = (rc[u] >> 1) & 1;                           // = the state phase 2 of t-1 derived from
+                                                            // R_t (S_t bit 4; iteration 1: the prologue)
       int ex, rbt;                                          // algorithms.py:105-109
       if constexpr (PAIRED) philox_decide(pbits[u], eps53, &ex, &rbt);
       else draw_pair<RNG>(a, rb, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
@@ -1205,7 +1220,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       sRn[ca] = (RT)rn;
       sRew[ca] = rew;  // (R_{t+1} is stored in phase 2: a store here would make the ring's
                        // record loads wait for it)
-      rc[u] |= act | (so << 1) | (s_t << 3);
+      rc[u] |= act | (AS ? so << 1 : 0);                    // (state and s_t bits: phase 1a)
       cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419 (D->C: finalize)
       cw1 += act == 0 ? one : 0u;
       const double am = act ? 0.0 : vmu;
@@ -1276,6 +1291,12 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint32_t gcn = 0, nmd2 = 0;  // group composition nibbles GC0..5; NMD_POS2
   if (acting) {
     double* pout = a.pub_out + (size_t)(rep * a.tiles_per_rep + tile) * PF * a.PB;
+    // border-record slots of this thread's agents (-1: interior or shadow slot), one 16-bit
+    // field per slot from the host table of the tile's shape: ~13 VALU per agent less than
+    // border_slot_or_none, and the load lands while the first agent is processed
+    // (border_slot_table: the host's build_ring_table)
+    const uint64_t bsw = *at(reinterpret_cast<const uint64_t*>(a.ring + (size_t)a.tiles_per_rep * a.ring_max),
+                             (uint32_t)(((th != a.TH ? 2 : 0) + (tw != a.TW ? 1 : 0)) * kBlock + tid));
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
@@ -1325,7 +1346,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
       const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
-      bmax = fmax(bmax, mdp);
+      bmax = max_f64(bmax, mdp);
       if (SPGG_ABLATE & 2048) {
       } else if constexpr (CODES) {
         st_stream(at(pendr, agent_of(rc[u])), (uint32_t)sCode[ca] | ((uint32_t)sCode[cbest] << 16));
@@ -1334,7 +1355,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
-      const int bslot = spgg_impl::border_slot_or_none(r, c, th, tw, HA);
+      const int bslot = (int)(int16_t)(uint16_t)(bsw >> (16 * u));  // (table: border_slot_table)
       if (bslot >= 0) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + bslot;
         rec[0] = sn ? q[u][2] : q[u][0];
@@ -1407,7 +1428,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     if (tid == 40 && acting) {  // lattice-wide max |diff| (spgg.py:488)
       double bm = 0.0;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) bm = fmax(bm, red[w * 64 + 12]);
+      for (int w = 0; w < kWaves; ++w) bm = max_f64(bm, red[w * 64 + 12]);
       // non-negative doubles order like their bit patterns
       if (bm > 0.0)
         atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
@@ -1871,7 +1892,25 @@ int build_ring_table(spgg_ctx* c) {
     const int th = std::min(c->TH, L - ty * c->TH), tw = std::min(c->TW, L - tx * c->TW);
     rmax = std::max(rmax, (tw + 2 * HA) * (th + 2 * HA) - th * tw);
   }
-  std::vector<int2> tab((size_t)c->tiles_per_rep * rmax, make_int2(0, 0));
+  // + the border-slot table (border_slot_table, kernel phase 2): per tile shape (th < TH: +2, tw < TW: +1) and
+  // thread, the border-record slot of each agent slot u < 4 (agent tid + u*kBlock), -1 for an
+  // interior cell or a slot past the tile (its shadow agent's owner writes the record)
+  std::vector<int2> tab((size_t)c->tiles_per_rep * rmax + 4 * kBlock, make_int2(0, 0));
+  {
+    const int ty_last = (L - 1) / c->TH, tx_last = (L - 1) / c->TW;
+    for (int shape = 0; shape < 4; ++shape) {
+      const int th = (shape & 2) ? L - ty_last * c->TH : c->TH, tw = (shape & 1) ? L - tx_last * c->TW : c->TW;
+      for (int tid = 0; tid < kBlock; ++tid) {
+        uint64_t w = 0;
+        for (int u = 0; u < 4; ++u) {
+          const int k = tid + u * kBlock;
+          const int slot = k < th * tw ? spgg_impl::border_slot_or_none(k / tw, k % tw, th, tw, HA) : -1;
+          w |= (uint64_t)(uint16_t)(int16_t)slot << (16 * u);
+        }
+        tab[(size_t)c->tiles_per_rep * rmax + shape * kBlock + tid] = make_int2((int)(uint32_t)w, (int)(uint32_t)(w >> 32));
+      }
+    }
+  }
   for (int tile = 0; tile < c->tiles_per_rep; ++tile) {
     const int ty = tile / c->tiles_x, tx = tile % c->tiles_x;
     const int y0 = ty * c->TH, x0 = tx * c->TW;

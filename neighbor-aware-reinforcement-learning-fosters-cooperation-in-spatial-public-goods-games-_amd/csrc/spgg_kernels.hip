@@ -237,21 +237,6 @@ using RStore = typename std::conditional<RQ, int8_t, double>::type;
 template <bool RQ>
 using RVal = typename std::conditional<RQ, int, double>::type;
 
-// The per-agent fields of spgg_rep_params, copied to LDS once per workgroup
-// (read through a reference into global memory the compiler must assume the
-// agents' stores may alias them and reloads them per agent).
-struct HotParams {
-  double norm_min, norm_den, norm_rcp, alpha, gamma, diag_alpha, diag_gamma;
-  double rep_gain_c, neg_delta_r_d, r_min, r_max, rep_unit;
-  int rk_gain, rk_loss, rk_min, rk_max;
-};
-
-__device__ __forceinline__ HotParams hot_params(const spgg_rep_params& p) {
-  return HotParams{p.norm_min, p.norm_den, p.norm_rcp, p.alpha, p.gamma, p.diag_alpha, p.diag_gamma,
-                   p.rep_gain_c, p.neg_delta_r_d, p.r_min, p.r_max, p.rep_unit, p.rk_gain, p.rk_loss, p.rk_min,
-                   p.rk_max};
-}
-
 template <bool RQ, typename PT>
 __device__ __forceinline__ RVal<RQ> rep_next(RVal<RQ> r, int act, const PT& p) {
   if constexpr (RQ) {  // spgg.py:321-323 in units of rep_unit
@@ -408,38 +393,45 @@ struct RowWindow {
   }
 };
 
+// x mod L for x in [-L, 2L) in four unsigned ops: min(x, x + L) takes x + L exactly when
+// x < 0 (x reads as a huge unsigned), min(y, y - L) takes y - L exactly when y >= L.
+__device__ __forceinline__ uint32_t wrap_once(int x, int L) {
+  const uint32_t y = min((uint32_t)x, (uint32_t)x + (uint32_t)L);
+  return min(y, y - (uint32_t)L);
+}
+
 // Window of h rows staged as aligned dwords (TWC kernels, L % 4 == 0, tile
 // columns multiples of 4): xb = the window's first global column rounded down
-// to a multiple of 4 (may be negative: periodic), DW dwords per row, flattened
-// over the workgroup (J >= h*DW / kBlock, host-checked via TH <= 25).  A
-// 46-byte row costs 12-13 lanes instead of 46 byte loads, one VGPR per J.
+// to a multiple of 4 (may be negative: periodic), DW dwords per row.  Thread t <
+// RPP*DW holds column t % DW of rows t / DW + j*RPP (RPP = kBlock / DW rows per
+// pass; J passes cover h, host-checked via TH <= 25), so the column, its wrap and
+// the first row are computed once and each pass adds a constant row (and a
+// constant LDS offset); rows and columns are wrapped by wrap_once.  A 46-byte row
+// costs 12-13 lanes instead of 46 byte loads, one VGPR per J.
 template <int J, int DW>
 struct DwordWindow {
+  static constexpr int RPP = kBlock / DW;
   uint32_t buf[J];
   __device__ __forceinline__ void load(const void* plane, int h, int y0, int xb, int L) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(plane);
-    const int tid = threadIdx.x, Ld = L >> 2, xd0 = xb >> 2;
+    const int tid = threadIdx.x, Ld = L >> 2;
+    const int r0 = tid / DW, col = tid - (tid / DW) * DW;  // idle threads (r0 >= RPP) load clamped rows
+    const uint32_t gx = wrap_once((xb >> 2) + col, Ld);
 #pragma unroll
     for (int j = 0; j < J; ++j) {  // unconditional loads (rows clamped)
-      const int k = tid + j * kBlock;
-      const int row = min(k / DW, h - 1), col = k - (k / DW) * DW;
-      int gy = y0 + row;
-      gy += gy < 0 ? L : 0;
-      gy -= gy >= L ? L : 0;
-      int gx = xd0 + col;
-      gx += gx < 0 ? Ld : 0;
-      gx -= gx >= Ld ? Ld : 0;
-      buf[j] = *at(src, __umul24((uint32_t)gy, (uint32_t)Ld) + (uint32_t)gx);  // gy, Ld < 2^24
+      const uint32_t gy = wrap_once(y0 + min(r0 + j * RPP, h - 1), L);
+      buf[j] = *at(src, __umul24(gy, (uint32_t)Ld) + gx);  // gy, Ld < 2^24
     }
   }
   // dst (pitch bytes, a multiple of 4): the window's dwords; dbit: bit0 of each byte.
   __device__ __forceinline__ void store(uint8_t* dst, int pitch, int h, uint8_t* dbit) {
     const int tid = threadIdx.x;
+    const int r0 = tid / DW, col = tid - (tid / DW) * DW;
+    const int o0 = r0 * pitch + col * 4;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int k = tid + j * kBlock;
-      if (k < h * DW) {
-        const int o = (k / DW) * pitch + (k - (k / DW) * DW) * 4;
+      if (r0 < RPP && r0 + j * RPP < h) {
+        const int o = o0 + j * RPP * pitch;
         *reinterpret_cast<uint32_t*>(dst + o) = buf[j];
         if (dbit) *reinterpret_cast<uint32_t*>(dbit + o) = buf[j] & 0x01010101u;
       }
@@ -672,12 +664,22 @@ __device__ __forceinline__ void select_row(const double (&q)[4], const double (&
     *v0 = s ? m10 : m00;
     *v1 = s ? m11 : m01;
   } else {
-    // the rows as opaque values: a select of two entries of q would otherwise be folded
-    // into one load at a computed index of q, which keeps q in scratch memory
-    double q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-    asm("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
-    *v0 = s ? q2 : q0;
-    *v1 = s ? q3 : q1;
+    // the row select written out (one compare, four 32-bit selects): as C++ selects of two
+    // entries of q it was folded into one load at a computed index of q, which keeps q in
+    // scratch memory (and an empty asm barrier on the entries cost four 64-bit copies)
+    uint32_t a0, a1, b0, b1;
+    asm("v_cmp_ne_u32_e32 vcc, 0, %4\n\t"
+        "v_cndmask_b32_e32 %0, %5, %6, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %7, %8, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %9, %10, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %11, %12, vcc"
+        : "=&v"(a0), "=&v"(a1), "=&v"(b0), "=&v"(b1)
+        : "v"(s), "v"(__double2loint(q[0])), "v"(__double2loint(q[2])), "v"(__double2hiint(q[0])),
+          "v"(__double2hiint(q[2])), "v"(__double2loint(q[1])), "v"(__double2loint(q[3])),
+          "v"(__double2hiint(q[1])), "v"(__double2hiint(q[3]))
+        : "vcc");
+    *v0 = __hiloint2double((int)a1, (int)a0);
+    *v1 = __hiloint2double((int)b1, (int)b0);
   }
 }
 
@@ -701,7 +703,7 @@ template <int ALG, int RNG, typename PT>
 __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size_t rb, int g, int t,
                                            uint32_t key, double eps, uint64_t eps53, bool diag, double rew,
                                            int so, int act, int sn, double (&q)[4],
-                                           double (&qb)[ALG == ALG_DQ ? 4 : 1]) {
+                                           double (&qb)[ALG == ALG_DQ ? 4 : 1], double* rn0, double* rn1) {
   const double alpha = pg.alpha, gamma = pg.gamma, dgamma = pg.diag_gamma;
   const int e = so * 2 + act;
   if constexpr (ALG == ALG_DQ) {
@@ -721,6 +723,8 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     const double nq1 = up1 ? u1 : qc1, nq2 = up1 ? qc2 : u2;
     q[0] = e == 0 ? nq1 : x0; q[1] = e == 1 ? nq1 : x1; q[2] = e == 2 ? nq1 : x2; q[3] = e == 3 ? nq1 : x3;
     qb[0] = e == 0 ? nq2 : y0; qb[1] = e == 1 ? nq2 : y1; qb[2] = e == 2 ? nq2 : y2; qb[3] = e == 3 ? nq2 : y3;
+    *rn0 = sn ? q[2] : q[0];
+    *rn1 = sn ? q[3] : q[1];
     return diag ? diag_td_dq(q, qb, e, sn, rew, pg) : 0.f;
   } else {
     // rows of the old and the new state; the updated entry is (so, act)
@@ -746,8 +750,10 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     q[1] = (!s1 && a1) ? q1 : q[1];
     q[2] = (s1 && !a1) ? q1 : q[2];
     q[3] = (s1 && a1) ? q1 : q[3];
-    if (!diag) return 0.f;
     const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];       // updated table, row s'
+    *rn0 = w0;  // (also the border record's row)
+    *rn1 = w1;
+    if (!diag) return 0.f;
     double target2;
     if constexpr (ALG == ALG_SARSA) {
       int ex, rbt;                                                   // diagnostic select, spgg.py:452
@@ -928,7 +934,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       // loads unconditional (threads without a u-th agent read the tile's
       // first one and drop it; md/atd are read even at t = 1, unused there):
       // conditional loads serialise on each other
-      const uint32_t g = own ? (uint32_t)((y0 + r) * L + (x0 + c)) : (uint32_t)(y0 * L + x0) + (TWC ? (tid & 1) : 0);
+      const uint32_t g = own ? g00 + __umul24((uint32_t)r, (uint32_t)L) + (uint32_t)c : g00 + (TWC ? (tid & 1) : 0);
       if (SPGG_ABLATE & 512) {  // compute-floor probe: no per-agent loads
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[u][k] = (double)((g + k) & 15) * 1e-3;
@@ -964,7 +970,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   constexpr int JRR = (25 + 2 * HA + kWaves - 1) / kWaves;
   constexpr int JSF = spgg_impl::js_of(M2), JRF = spgg_impl::jr_of();
   constexpr int DWS = (TWC + 2 * HS + 3 + 3) / 4, DWR = (TWC + 2 * HA + 3 + 3) / 4;
-  constexpr int JSD = ((25 + 2 * HS) * DWS + kBlock - 1) / kBlock, JRD = ((25 + 2 * HA) * DWR + kBlock - 1) / kBlock;
+  constexpr int JSD = (25 + 2 * HS + kBlock / DWS - 1) / (kBlock / DWS);  // passes of kBlock / DW rows
+  constexpr int JRD = (25 + 2 * HA + kBlock / DWR - 1) / (kBlock / DWR);
   // window column j lives at plane column j + its misalignment (views below)
   const int soffS = TWC ? ((x0 - HS) & 3) : 0, soffR = TWC && RQ ? ((x0 - HA) & 3) : 0;
   uint8_t* sSv = sS + soffS;  // S / defector planes indexed by window coordinates
@@ -985,16 +992,19 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const int st = a.stop_iter[rep];
   const bool dead = st != 0 && st < t;  // absorbed before t: nothing to do
   const spgg_rep_params& pg = a.params[rep];
-  __shared__ HotParams hps;  // per-agent fields in LDS (written before the staging barrier)
-  if (tid == 0) hps = hot_params(pg);
-  const HotParams& hp = hps;
-  if (tid == 0) {  // scalar loads of the replica's payoff tables, indexed by defector count
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      tab[k] = pg.pay_c[5 - k];
-      tab[6 + k] = pg.pay_d[5 - k];
-    }
-  }
+  // the replica's parameters (per-agent fields read from LDS: through a reference into global
+  // memory the compiler must assume the agents' stores alias them) and its payoff tables
+  // indexed by defector count, one 8-byte word per thread (a one-lane copy took ~40 VALU
+  // moves of one wave); loaded unconditionally (clamped) with the windows, stored with them
+  __shared__ spgg_rep_params hps;
+  static_assert(sizeof(spgg_rep_params) % 8 == 0, "spgg_rep_params: whole 8-byte words");
+  constexpr int kParamWords = (int)(sizeof(spgg_rep_params) / 8);
+  constexpr int kPayWord = (int)(offsetof(spgg_rep_params, pay_c) / 8);  // pay_d follows pay_c
+  const uint64_t pword = *at(reinterpret_cast<const uint64_t*>(&pg),
+                             (uint32_t)(tid < kParamWords ? tid
+                                        : tid < kParamWords + 6 ? kPayWord + 5 - (tid - kParamWords)
+                                        : kPayWord + 17 - min(tid - kParamWords, 11)));
+  const spgg_rep_params& hp = hps;
   const double kappa = pg.kappa, w_p = pg.w_p, w_rep = pg.w_rep;
   // the replica's history record: slot values are sums over its stripes (max for GMAX);
   // this workgroup adds to stripe tile % stripes (bounded atomic contention per address)
@@ -1022,6 +1032,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 
   if (SPGG_PRIO) __builtin_amdgcn_s_setprio(0);
   // windows -> LDS (waits for the loads above)
+  if (tid < kParamWords) reinterpret_cast<uint64_t*>(&hps)[tid] = pword;
+  else if (tid < kParamWords + 12) reinterpret_cast<uint64_t*>(tab)[tid - kParamWords] = pword;
   if constexpr (TWC > 0) {
     winS.store(sS, ly.sw, th + 2 * HS, sD);
     if constexpr (!AS) {
@@ -1297,6 +1309,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     // (border_slot_table: the host's build_ring_table)
     const uint64_t bsw = *at(reinterpret_cast<const uint64_t*>(a.ring + (size_t)a.tiles_per_rep * a.ring_max),
                              (uint32_t)(((th != a.TH ? 2 : 0) + (tw != a.TW ? 1 : 0)) * kBlock + tid));
+    // the stored diagnostic |alpha*td'| (kappa == 0: the NI percent it feeds is exactly 0), as a
+    // scalar flag (an f64 compare has no scalar form and was repeated on the VALU per agent)
+    const bool diag_on = ATD && __builtin_amdgcn_readfirstlane((int)(kappa != 0.0)) != 0;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
@@ -1308,9 +1323,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
       // (the diagnostic only where it is stored; with reward codes the next launch recomputes it)
-      const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, ATD && kappa != 0.0,
-                                            rew, so, act, sn, q[u], qb[u]);
-      if (ATD && kappa != 0.0 && !(SPGG_ABLATE & (256 | 2048))) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
+      double rn0, rn1;  // row s_{t+1} of the updated table (the border record's)
+      const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, diag_on, rew, so,
+                                            act, sn, q[u], qb[u], &rn0, &rn1);
+      if (diag_on && !(SPGG_ABLATE & (256 | 2048))) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
       if (!(SPGG_ABLATE & 2048)) {
         // entry the NI term of t-1 changed in phase 1a (none at t = 1 or with kappa == 0)
         const int e_old = (pending && kappa != 0.0) ? pending_entry(sSv[(r + HS) * ly.sw + (c + HS)]) : -1;
@@ -1339,7 +1355,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       for (int kk = 1; kk < KN; ++kk) {
         const double d = rw[kk] - rew;
         const bool better = d > md;
-        md = better ? d : md;
+        md = max_f64(md, d);  // = better ? d : md (equal values are equal doubles: rewards are never -0)
         abest = better ? an[kk] : abest;
         if constexpr (CODES) cbest = better ? nb[kk] : cbest;
         if constexpr (M2) ks = better ? kk : ks;
@@ -1358,8 +1374,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int bslot = (int)(int16_t)(uint16_t)(bsw >> (16 * u));  // (table: border_slot_table)
       if (bslot >= 0) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + bslot;
-        rec[0] = sn ? q[u][2] : q[u][0];
-        rec[a.PB] = sn ? q[u][3] : q[u][1];
+        rec[0] = rn0;
+        rec[a.PB] = rn1;
         if constexpr (QB) {
           rec[2 * a.PB] = sn ? qb[u][QB ? 2 : 0] : qb[u][0];
           rec[3 * a.PB] = sn ? qb[u][QB ? 3 : 0] : qb[u][QB ? 1 : 0];

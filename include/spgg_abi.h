@@ -160,7 +160,10 @@ typedef struct {
  *                                    max(0, max_diff) of every agent within M cells of
  *                                    its tile's edge, read by the neighbouring tiles
  *   md        f64    [n_rep][n]      max(0, max_diff) of the pending iteration, in place
+ *                                    (kept only for replicas with kappa != 0: the NI term it
+ *                                    feeds is +0 otherwise)
  *   atd       f32    [n_rep][n]      |alpha*td'| of the pending iteration (diagnostic), in place
+ *                                    (likewise only for kappa != 0)
  *   draws     uint8  [planes][..][n] the step's random draws as 0/1 bytes (INJECT/MT19937),
  *                                    one plane per draw of the reference, in its order
  *                                    (spgg_draw_planes): plane 2k = (rand < eps) and
@@ -205,7 +208,9 @@ const char* spgg_last_error(const spgg_ctx* ctx);
 /* Environment knob read here: SPGG_APT = "1" (one agent per thread) or "max" (the
  * operator's maximum) forces the tiling; any other value fails with SPGG_E_ARG. */
 int spgg_create(spgg_ctx** out, const spgg_config* cfg);
-/* Copies n_rep host records to the device (stream-ordered on the null stream). */
+/* Copies n_rep host records to the device (stream-ordered on the null stream).  Between
+ * spgg_step calls of one run a replica's kappa must not change from 0 to nonzero (the pending
+ * max_diff / |alpha*td'| records of kappa == 0 replicas are not kept). */
 int spgg_set_params(spgg_ctx* ctx, const spgg_rep_params* params);
 int spgg_bind(spgg_ctx* ctx, const spgg_buffers* bufs);
 

@@ -1311,7 +1311,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                              (uint32_t)(((th != a.TH ? 2 : 0) + (tw != a.TW ? 1 : 0)) * kBlock + tid));
     // the stored diagnostic |alpha*td'| (kappa == 0: the NI percent it feeds is exactly 0), as a
     // scalar flag (an f64 compare has no scalar form and was repeated on the VALU per agent)
-    const bool diag_on = ATD && __builtin_amdgcn_readfirstlane((int)(kappa != 0.0)) != 0;
+    const bool ni_on = __builtin_amdgcn_readfirstlane((int)(kappa != 0.0)) != 0;
+    const bool diag_on = ATD && ni_on;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
@@ -1367,7 +1368,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       } else if constexpr (CODES) {
         st_stream(at(pendr, agent_of(rc[u])), (uint32_t)sCode[ca] | ((uint32_t)sCode[cbest] << 16));
       } else {
-        st_stream(at(mdr, agent_of(rc[u])), mdp);
+        // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
+        // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)
+        if (ni_on) st_stream(at(mdr, agent_of(rc[u])), mdp);
       }
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
@@ -1380,7 +1383,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
           rec[2 * a.PB] = sn ? qb[u][QB ? 2 : 0] : qb[u][0];
           rec[3 * a.PB] = sn ? qb[u][QB ? 3 : 0] : qb[u][QB ? 1 : 0];
         }
-        rec[(PF - 1) * a.PB] = mdp;
+        if (ni_on) rec[(PF - 1) * a.PB] = mdp;
       }
       // group composition on S_{t+1}, spgg.py:585-592: nibble nd of gcn
       const int nd = act + an[0] + an[1] + an[2] + an[3];   // (the four axial neighbours, loaded above)

@@ -210,7 +210,8 @@ const char* spgg_last_error(const spgg_ctx* ctx);
 int spgg_create(spgg_ctx** out, const spgg_config* cfg);
 /* Copies n_rep host records to the device (stream-ordered on the null stream).  Between
  * spgg_step calls of one run a replica's kappa must not change from 0 to nonzero (the pending
- * max_diff / |alpha*td'| records of kappa == 0 replicas are not kept). */
+ * max_diff / |alpha*td'| records of kappa == 0 replicas are not kept): a later spgg_step with
+ * t0 > 1 then fails with SPGG_E_STATE (t0 == 1 starts a new run). */
 int spgg_set_params(spgg_ctx* ctx, const spgg_rep_params* params);
 int spgg_bind(spgg_ctx* ctx, const spgg_buffers* bufs);
 

@@ -1836,6 +1836,8 @@ struct spgg_ctx {
   spgg_buffers buf{};
   bool bound = false;
   bool params_set = false;
+  std::vector<double> kappa_host;  // the replicas' kappa as last set
+  bool kappa_woke = false;         // a kappa went 0 -> nonzero since the run's iteration 1
   spgg_rep_params* d_params = nullptr;
   int2* d_ring = nullptr;   // ring table (geometry of the tiling)
   int ring_max = 0;
@@ -2140,6 +2142,12 @@ int spgg_set_params(spgg_ctx* c, const spgg_rep_params* params) {
   }
   rc = hip_check(c, hipMemcpy(c->d_params, params, bytes, hipMemcpyHostToDevice), "hipMemcpy(params)");
   if (rc) return rc;
+  // kappa == 0 replicas keep no pending NI record (md / atd): continuing a run after one of them
+  // turned nonzero would read records that were never written (spgg_step refuses it)
+  if (c->kappa_host.size() == (size_t)c->cfg.n_rep)
+    for (int r = 0; r < c->cfg.n_rep; ++r) c->kappa_woke |= c->kappa_host[r] == 0.0 && params[r].kappa != 0.0;
+  c->kappa_host.resize(c->cfg.n_rep);
+  for (int r = 0; r < c->cfg.n_rep; ++r) c->kappa_host[r] = params[r].kappa;
   c->params_set = true;
   return SPGG_OK;
 }
@@ -2170,6 +2178,9 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
     return fail(c, SPGG_E_ARG, "spgg_step: iteration range outside [1, iterations]");
   if (c->cfg.rng_mode == SPGG_RNG_INJECT && n_steps > 1)
     return fail(c, SPGG_E_ARG, "spgg_step: INJECT mode steps one iteration per call");
+  if (t0 == 1) c->kappa_woke = false;  // a new run
+  else if (c->kappa_woke)
+    return fail(c, SPGG_E_STATE, "spgg_step: a replica's kappa changed from 0 to nonzero mid-run");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
   for (int t = t0; t < t0 + n_steps; ++t) {

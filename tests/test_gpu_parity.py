@@ -529,3 +529,28 @@ def test_philox_results_independent_of_tiling(M2, state, monkeypatch):
     # history records: the same values summed over different tile partitions (f32 NI-percent
     # partials per workgroup): equal to rounding, far inside the 1e-5 history tolerance
     np.testing.assert_allclose(res["1"][2], res["max"][2], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_kappa_woken_mid_run_is_refused():
+    """A kappa == 0 replica keeps no pending NI record (max_diff, |alpha*td'|), so continuing a
+    run after its kappa turned nonzero is refused (include/spgg_abi.h spgg_set_params); the same
+    change before iteration 1 of a new run is accepted."""
+    import ctypes
+    from spgg_amd import _lib as C
+    eng = BatchEngine(24, 10, [_runner_params(seed=0, influence_factor=0.0)], use_second_order=False,
+                      rng="philox")
+    try:
+        eng.step(3)
+        g = eng.groups[0]
+        p = _runner_params(seed=0, influence_factor=1.0).to_c()
+        p.stream_id = 0
+        C.check(eng.lib.spgg_set_params(g["ctx"], (C.RepParams * 1)(p)), g["ctx"], "spgg_set_params")
+        rc = eng.lib.spgg_step(g["ctx"], 4, 1, ctypes.c_void_p(eng.stream))
+        assert rc == C.E_STATE, rc
+        assert b"kappa" in eng.lib.spgg_last_error(g["ctx"])
+        # a new run (t0 = 1) with the new kappa is fine
+        assert eng.lib.spgg_step(g["ctx"], 1, 1, ctypes.c_void_p(eng.stream)) == C.OK
+        torch.cuda.synchronize()
+    finally:
+        eng.close()

@@ -56,6 +56,9 @@ def workload(name, rank):
     if name == "cfg5":
         return ("cfg5: L=1000 r=3.6 kappa=1.0 M=1 reputation, 1 replica per GPU", 1000, False, "reputation",
                 [runner_params(r=3.6, influence_factor=1.0, seed=off)])
+    if name == "run100":  # the shape one SPGG(...).run() of the reference's runner steps (runner.py:88-101)
+        return ("run100: L=100 r=3.0 kappa=1.0 M=1 reputation, 1 replica (one SPGG.run of the runner)", 100,
+                False, "reputation", [runner_params(r=3.0, influence_factor=1.0, seed=off)])
     raise SystemExit(f"unknown config {name}")
 
 
@@ -152,7 +155,7 @@ def main():
     K, W = args.steps, args.warmup
     T = K + W
     eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng,
-                      streams=args.streams)
+                      streams=args.streams, replica_offset=rank * len(reps))
     n_agents = len(reps) * L * L
 
     eng.step(W)

@@ -125,7 +125,9 @@ typedef struct {
   double r_min;
   double r_max;
   uint64_t seed;      /* Philox key (SPGG_RNG_PHILOX only) */
-  uint64_t stream_id; /* Philox stream: global replica id (independent of batching) */
+  uint64_t stream_id; /* Philox stream: the caller's GLOBAL replica index (BatchEngine: its
+                         replica_offset, a rank's shard start, + k), so a replica draws the
+                         same stream whatever the batching or world size */
   /* group payoff of a cooperator / defector in a group with N cooperators,
    * N = 0..5: (r*c*N)/5 - cost and (r*c*N)/5 (spgg.py:256-257), computed by
    * the host in the reference's order. */
@@ -211,7 +213,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg);
 /* Copies n_rep host records to the device (stream-ordered on the null stream).  Between
  * spgg_step calls of one run a replica's kappa must not change from 0 to nonzero (the pending
  * max_diff / |alpha*td'| records of kappa == 0 replicas are not kept): a later spgg_step with
- * t0 > 1 then fails with SPGG_E_STATE (t0 == 1 starts a new run). */
+ * t0 > 1, or spgg_flush, then fails with SPGG_E_STATE (spgg_step with t0 == 1 starts a new run). */
 int spgg_set_params(spgg_ctx* ctx, const spgg_rep_params* params);
 int spgg_bind(spgg_ctx* ctx, const spgg_buffers* bufs);
 
@@ -222,7 +224,9 @@ int spgg_bind(spgg_ctx* ctx, const spgg_buffers* bufs);
 int spgg_step(spgg_ctx* ctx, int32_t t0, int32_t n_steps, void* hip_stream);
 
 /* Apply the deferred neighbor-influence term of iteration t_last (the last
- * executed one) and its Q statistics.  Call once after the final spgg_step. */
+ * executed one) and its Q statistics.  Call once after the final spgg_step.
+ * SPGG_E_STATE if a replica's kappa went from 0 to nonzero since the run began
+ * (its pending record was never written; see spgg_set_params). */
 int spgg_flush(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
 
 /* Fill the derived history slots (SPGG_ST_SUMP / _SUMP_C / _SUMP_D of iterations 1..last,

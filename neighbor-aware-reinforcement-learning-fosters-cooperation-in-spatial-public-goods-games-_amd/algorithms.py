@@ -7,6 +7,13 @@ factory with its ValueError.  Their per-lattice `select_action` /
 driven by `SPGG.run` / `BatchEngine`; calling those two methods on their own
 raises, because this package has no NumPy execution path by design.
 
+The plug-in point (`SPGG(algorithm=<RLAlgorithm instance>)`, spgg.py:111-118):
+`operator_kind` accepts these four classes, the reference's own four (an
+instance built from src/model/algorithms.py drops in) and subclasses that only
+add state; anything that redefines the operator's methods is refused with a
+ValueError naming the class, so custom arithmetic can never silently run as the
+built-in operator.
+
 GPU coverage: all four operators -- QLearning (algorithms.py:96-133), SARSA
 (:136-178), ExpectedSARSA (:181-234), DoubleQLearning (:237-341) -- each a
 template instance of the step kernel (spgg_kernels.hip, SPGG_ALG_*).
@@ -87,12 +94,68 @@ _ALIASES = {"qlearning": "qlearning", "q-learning": "qlearning", "sarsa": "sarsa
             "expected_sarsa": "expected_sarsa", "expected-sarsa": "expected_sarsa",
             "double_qlearning": "double_qlearning", "double-q-learning": "double_qlearning"}
 
+# The reference's operator classes (algorithms.py:96, 136, 181, 237) by class name.
+_BUILTIN_CLASSES = {"QLearning": "qlearning", "SARSA": "sarsa", "ExpectedSARSA": "expected_sarsa",
+                    "DoubleQLearning": "double_qlearning"}
+# Methods whose arithmetic the device step reproduces: a class that redefines any of them
+# computes something the HIP kernels do not (algorithms.py:40-93, 250-341).
+_FUSED_METHODS = ("select_action", "update_q_table", "decay_epsilon", "initialize_q_tables",
+                  "get_combined_q_table")
+_HYPER = ("alpha", "gamma", "epsilon", "epsilon_decay", "epsilon_min")
+
+
+def operator_kind(algorithm) -> str:
+    """Operator kind of an RLAlgorithm instance -- the reference's plug-in point
+    (spgg.py:111-118) -- or ValueError when the device step cannot run it.
+
+    Accepted: this module's four operator classes, the reference's own four
+    (src/model/algorithms.py, matched by class name and module, so an instance built
+    from the reference package drops in), and subclasses of either that add state
+    but redefine none of the operator's methods.  A subclass that overrides
+    select_action / update_q_table / decay_epsilon (or Double-Q's table methods), or
+    an RLAlgorithm that derives from none of the four, defines arithmetic the HIP
+    step does not contain: it is refused here rather than silently replaced by the
+    built-in operator's math."""
+    cls = type(algorithm)
+    base = None
+    for k in cls.__mro__:
+        if k.__module__.split(".")[-1] == "algorithms" and k.__name__ in _BUILTIN_CLASSES:
+            base = k
+            break
+        if k.__name__ == "RLAlgorithm" or k is object:
+            break
+        redefined = [m for m in _FUSED_METHODS if m in vars(k)]
+        if redefined:
+            raise ValueError(
+                f"algorithm {cls.__module__}.{cls.__qualname__}: {k.__qualname__} redefines "
+                f"{', '.join(redefined)}; the MI355X step fuses the reference operators' own "
+                f"select_action/update_q_table arithmetic (QLearning, SARSA, ExpectedSARSA, "
+                f"DoubleQLearning) and cannot run a custom operator")
+    if base is None:
+        raise ValueError(
+            f"algorithm {cls.__module__}.{cls.__qualname__} is not one of the operators the MI355X "
+            f"step implements (QLearning, SARSA, ExpectedSARSA, DoubleQLearning or a subclass that "
+            f"keeps their methods)")
+    missing = [h for h in _HYPER if not hasattr(algorithm, h)]
+    if missing:
+        raise ValueError(f"algorithm {cls.__qualname__} lacks {', '.join(missing)}")
+    return _BUILTIN_CLASSES[base.__name__]
+
+
+def is_operator(algorithm) -> bool:
+    """An RLAlgorithm of this package or an instance of the reference's RLAlgorithm
+    hierarchy (duck-typed by class name: the reference package is not imported)."""
+    if isinstance(algorithm, RLAlgorithm):
+        return True
+    return any(k.__name__ == "RLAlgorithm" and k.__module__.split(".")[-1] == "algorithms"
+               for k in type(algorithm).__mro__)
+
 
 def canonical_name(algorithm) -> str:
     """Operator kind of a name (create_algorithm's accepted spellings, algorithms.py:371-383)
-    or of an RLAlgorithm instance."""
-    if isinstance(algorithm, RLAlgorithm):
-        return algorithm.kind
+    or of an RLAlgorithm instance (operator_kind)."""
+    if not isinstance(algorithm, str) and is_operator(algorithm):
+        return operator_kind(algorithm)
     name = str(algorithm).lower()
     if name not in _ALIASES:
         raise ValueError(f"Unknown algorithm: {name}. "

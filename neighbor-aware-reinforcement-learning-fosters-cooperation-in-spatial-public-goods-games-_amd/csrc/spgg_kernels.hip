@@ -1243,7 +1243,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       sRew[ca] = rew;  // (R_{t+1} is stored in phase 2: a store here would make the ring's
                        // record loads wait for it)
       rc[u] |= act | (AS ? so << 1 : 0);                    // (state and s_t bits: phase 1a)
-      cw0 += (s_t == 0 && act == 1) ? one : 0u;            // spgg.py:419 (D->C: finalize)
+      cw0 += (s_t == 0 && act == 1) ? one : 0u;            // C->D, spgg.py:419 (D->C is derived
+                                                            // in spgg_history_finalize)
       cw1 += act == 0 ? one : 0u;
       const double am = act ? 0.0 : vmu;
       va[1] = __builtin_fma(rew, am, va[1]);                // spgg.py:542
@@ -1445,14 +1446,15 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int j = tid - 16;  // 0-2 va, 3-13 counters
       // record index of value j, one byte each in two 64-bit immediates (a
       // constant-memory table would cost the epilogue a memory round trip)
+      // (j = 4, cw0's high half, counts nothing: SW_DC is written by spgg_history_finalize alone)
       constexpr uint64_t km0 = stat_bytes(SPGG_ST_SUMR, SPGG_ST_SUM_REW_C, SPGG_ST_SUM_RATIO_C, SPGG_ST_SW_CD,
-                                          SPGG_ST_SW_DC, SPGG_ST_NCOOP, SPGG_ST_NMD_POS, SPGG_ST_NMD_POS2);
+                                          -1, SPGG_ST_NCOOP, SPGG_ST_NMD_POS, SPGG_ST_NMD_POS2);
       constexpr uint64_t km1 = stat_bytes(SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2, SPGG_ST_GC0 + 3,
                                           SPGG_ST_GC0 + 4, SPGG_ST_GC0 + 5, -1, -1);
       k = (int)(int8_t)(uint8_t)((j < 8 ? km0 : km1) >> (8 * (j & 7)));
       src = 16 + j;
       const bool start_val = j == 0;                   // recorded on the absorbing iteration too
-      if (acting || start_val) slot = (j == 5) ? t + 1 : t;
+      if ((acting || start_val) && k >= 0) slot = (j == 5) ? t + 1 : t;
     }
     if (tid == 40 && acting) {  // lattice-wide max |diff| (spgg.py:488)
       double bm = 0.0;
@@ -2194,6 +2196,8 @@ int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {
   if (!c) return SPGG_E_ARG;
   if (!c->bound || !c->params_set) return fail(c, SPGG_E_STATE, "spgg_flush before bind/set_params");
   if (t_last < 1 || t_last > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_flush: bad t_last");
+  if (c->kappa_woke)  // the NI term would read a pending record that was never written
+    return fail(c, SPGG_E_STATE, "spgg_flush: a replica's kappa changed from 0 to nonzero mid-run");
   launch_step(c, t_last + 1, 1, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_flush launch");
 }

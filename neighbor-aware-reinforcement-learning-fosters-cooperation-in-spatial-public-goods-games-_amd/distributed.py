@@ -12,10 +12,44 @@ tensors, "gloo" for the CPU tests.
 """
 from __future__ import annotations
 
-from typing import Sequence
+import os
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
+
+
+def local_device() -> Optional[int]:
+    """Select this process's GPU before any engine or communicator exists: LOCAL_RANK
+    under torchrun (one rank per GPU), else GPU 0.  None without a GPU (CPU / gloo)."""
+    if not torch.cuda.is_available():
+        return None
+    d = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(d)
+    return d
+
+
+def init_from_env(backend: Optional[str] = None) -> bool:
+    """Initialise torch.distributed from torchrun's environment (WORLD_SIZE, RANK,
+    LOCAL_RANK, MASTER_ADDR/PORT) when WORLD_SIZE > 1 and no group exists yet.
+
+    The GPU is selected first (local_device), so the RCCL communicator binds to this
+    rank's device.  backend: $SPGG_DIST_BACKEND, else "nccl" (RCCL on ROCm) with a GPU
+    and "gloo" without.  Returns True when this call created the group (the caller
+    destroys it)."""
+    import torch.distributed as dist
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return False
+    backend = backend or os.environ.get("SPGG_DIST_BACKEND")
+    dev = local_device()
+    if backend is None:
+        backend = "nccl" if dev is not None else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group(backend)
+    return True
 
 
 def shard_range(n_items: int, world: int, rank: int):
@@ -79,17 +113,26 @@ def run_sharded(replicas, L: int, iterations: int, use_second_order=True,
                 state_representation="reputation", rng="mt19937", device=None, group=None):
     """Run this rank's block of `replicas` on its GPU, then all-gather the summaries.
 
-    Returns (summaries (N, 4) on every rank, this rank's BatchEngine)."""
+    The rank's GPU is LOCAL_RANK (torchrun) unless `device` names one; replica k of
+    the block keeps its global index (shard offset + k) as its Philox stream id, so a
+    replica's stream -- and its trajectory in "philox" mode -- does not depend on the
+    world size.  Returns (summaries (N, 4) on every rank, this rank's BatchEngine)."""
     import torch.distributed as dist
-    from .engine import BatchEngine
+    from . import engine as E
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    mine = shard(replicas, world, rank)
+    if device is None:
+        device = local_device()
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(device)
+    a, b = shard_range(len(replicas), world, rank)
+    mine = list(replicas[a:b])
     eng = None
     local = np.zeros((0, len(SUMMARY_FIELDS)))
     if mine:
-        eng = BatchEngine(L, iterations, mine, use_second_order=use_second_order,
-                          state_representation=state_representation, rng=rng, device=device)
+        eng = E.BatchEngine(L, iterations, mine, use_second_order=use_second_order,
+                            state_representation=state_representation, rng=rng, device=device,
+                            replica_offset=a)
         eng.run(snapshots=False)
         local = replica_summaries(eng)
     if world == 1:

@@ -192,7 +192,7 @@ class BatchEngine:
                  use_second_order: bool = True, state_representation: str = "reputation",
                  rng: str = "mt19937", device=None, init: Optional[Sequence[InitState]] = None,
                  lib_path: Optional[str] = None, streams: Optional[int] = None,
-                 algorithm: str = "qlearning"):
+                 algorithm: str = "qlearning", replica_offset: int = 0):
         if state_representation not in ("reputation", "action"):
             raise ValueError(f"Unknown state_representation: {state_representation}. "
                              f"Must be 'reputation' or 'action'")
@@ -212,6 +212,9 @@ class BatchEngine:
         self.M2 = bool(use_second_order)
         self.state_rep = state_representation
         self.rng = rng
+        # global index of replica 0 (a rank's shard offset): replica k's Philox stream id is
+        # replica_offset + k, so its stream does not depend on how the sweep was sharded
+        self.replica_offset = int(replica_offset)
         self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         if init is None:
             init = [reference_init(self.L, np.random.RandomState(p.seed), algorithm=self.algorithm)
@@ -308,7 +311,7 @@ class BatchEngine:
                        algorithm=self.alg, batch_reps=self.R)   # one tiling for every group
         params = [p.to_c() for p in self.reps]
         for k, p in enumerate(params):
-            p.stream_id = k
+            p.stream_id = self.replica_offset + k
         self.groups = []
         if self.G == 1:
             streams = [torch.cuda.current_stream(self.dev)]

@@ -52,7 +52,11 @@ class SPGG:
         if isinstance(algorithm, str):
             self.algorithm = A.create_algorithm(algorithm, alpha, gamma, epsilon,
                                                 epsilon_decay, epsilon_min, **params)
-        elif isinstance(algorithm, A.RLAlgorithm):
+        elif A.is_operator(algorithm):
+            # the plug-in point (spgg.py:115-116): one of the operators the device step
+            # implements, this package's or the reference's own; a custom operator raises
+            # ValueError here instead of running the built-in math (algorithms.operator_kind)
+            A.operator_kind(algorithm)
             self.algorithm = algorithm
         else:
             raise ValueError(f"algorithm must be str or RLAlgorithm, got {type(algorithm)}")

@@ -306,11 +306,14 @@ def run_experiments(param_combinations: List[Tuple], num_processes: Optional[int
             bar.refresh()
 
     import torch.distributed as dist
+    from .distributed import local_device
     try:
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             world, rank = dist.get_world_size(), dist.get_rank()
             a, b = shard_range(len(params), world, rank)
-            local = run_batch(params[a:b], seeds[a:b], save_png=save_png, progress=progress, **model_overrides)
+            # this rank's GPU (LOCAL_RANK), before its engine exists; only its own block runs here
+            local = run_batch(params[a:b], seeds[a:b], device=local_device(), save_png=save_png,
+                              progress=progress, **model_overrides)
             rows = np.array([[res[0], res[1]] for _, res in local], dtype=np.float64).reshape(-1, 2)
             dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else None
             allr = gather_rows(rows, len(params), device=dev)
@@ -368,10 +371,24 @@ def main(argv=None):
     config = load_config(args.config)
     algs = resolve_algorithms(args.algorithms, config)
     combos = [(*p, a) for p in generate_param_combinations(config, args.experiment_type) for a in algs]
-    print(f"Algorithms selected: {', '.join(algs)}")
-    print(f"Total parameter combinations: {len(combos)}")
-    results = run_experiments(combos, num_processes=args.num_processes, use_progress_bar=not args.no_progress)
-    print(f"\nCompleted {len(results)} experiments")
+    # under torchrun (WORLD_SIZE > 1): one rank per GPU, each running its block of the
+    # tuples (run_experiments' distributed branch), instead of every rank fanning out
+    # over all GPUs
+    from .distributed import init_from_env
+    import torch.distributed as dist
+    owned = init_from_env()
+    lead = not dist.is_initialized() or dist.get_rank() == 0
+    try:
+        if lead:
+            print(f"Algorithms selected: {', '.join(algs)}")
+            print(f"Total parameter combinations: {len(combos)}")
+        results = run_experiments(combos, num_processes=args.num_processes,
+                                  use_progress_bar=lead and not args.no_progress)
+        if lead:
+            print(f"\nCompleted {len(results)} experiments")
+    finally:
+        if owned:
+            dist.destroy_process_group()
     return results
 
 

@@ -549,6 +549,10 @@ def test_kappa_woken_mid_run_is_refused():
         rc = eng.lib.spgg_step(g["ctx"], 4, 1, ctypes.c_void_p(eng.stream))
         assert rc == C.E_STATE, rc
         assert b"kappa" in eng.lib.spgg_last_error(g["ctx"])
+        # nor may the run be flushed: the flush's NI term would read the unwritten record
+        rc = eng.lib.spgg_flush(g["ctx"], 3, ctypes.c_void_p(eng.stream))
+        assert rc == C.E_STATE, rc
+        assert b"kappa" in eng.lib.spgg_last_error(g["ctx"])
         # a new run (t0 = 1) with the new kappa is fine
         assert eng.lib.spgg_step(g["ctx"], 1, 1, ctypes.c_void_p(eng.stream)) == C.OK
         torch.cuda.synchronize()

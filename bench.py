@@ -72,15 +72,27 @@ def cpu_baseline(L, M2, state, reps, budget_s=15.0):
     import multiprocessing as mp
     procs = max(1, min(16, os.cpu_count() or 1, len(reps)))
     jobs = [(L, M2, state, reps[i % len(reps)], budget_s) for i in range(procs)]
-    with mp.get_context("fork").Pool(procs) as pool:
+    # spawned (not forked) workers: the parent holds a HIP context; the workers are NumPy only
+    with mp.get_context("spawn").Pool(procs) as pool:
         done = pool.map(_cpu_job, jobs)
     steps = sum(d[0] for d in done)
     wall = max(d[1] for d in done)
     agent_steps = steps * L * L
-    return {"value": agent_steps / wall, "unit": "agent-steps/s", "cores": procs, "kind": "port",
-            "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics), {procs} processes, each stepping "
-                      f"one L={L} replica of the same workload for {budget_s:.0f} s after 3 warm-up "
-                      f"iterations; {steps} iterations in {wall:.1f} s wall"}
+    out = {"value": agent_steps / wall, "unit": "agent-steps/s", "cores": procs, "kind": "port",
+           "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics), {procs} processes, each stepping "
+                     f"one L={L} replica of the same workload for {budget_s:.0f} s after 3 warm-up "
+                     f"iterations; {steps} iterations in {wall:.1f} s wall"}
+    # the oracle's speed relative to the reference's own SPGG.run on the same core
+    # (tools/calibrate_cpu.py, survey container; the reference never travels)
+    cal = os.path.join(ROOT, "profiles", "r03", "cpu_calibration.json")
+    if os.path.exists(cal):
+        c = json.load(open(cal))
+        out["oracle_over_reference"] = c["oracle_over_reference"]
+        out["reference_equivalent_value"] = out["value"] / c["oracle_over_reference"]
+        out["calibration"] = (f"profiles/r03/cpu_calibration.json: {c['workload']}; reference "
+                              f"{c['reference_ms_per_iteration']:.1f} ms/iteration vs oracle "
+                              f"{c['oracle_ms_per_iteration']:.1f}, one core of {c['cpu']}")
+    return out
 
 
 class _Budget(Exception):
@@ -116,6 +128,35 @@ def _cpu_job(job):
     return clock["n"], time.perf_counter() - clock["t0"]
 
 
+FULL_RUN_ITERS = {"cfg2": 10000, "cfg3": 10000, "cfg4": 10000, "cfg5": 100000, "run100": 100001}
+
+
+def full_run(L, M2, state, reps, rng, streams, T, offset):
+    """The configuration's whole run (BASELINE.json iterations) as a user runs it:
+    BatchEngine.run() -- absorbing replicas, group retirement, host syncs every 256
+    iterations, the final flush -- timed from the first launch to the flush."""
+    import numpy as np
+    import torch
+    from spgg_amd.engine import BatchEngine
+    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=rng, streams=streams,
+                      replica_offset=offset)
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.run(snapshots=False)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        stop = eng.stopped
+        executed = np.where(stop == 0, eng.t - 1, stop - 1).astype(np.int64)
+        absorbed = int(np.sum(stop != 0))
+    finally:
+        eng.close()
+    agent_steps = float(executed.sum()) * L * L
+    return {"iterations": T, "value": agent_steps / wall, "unit": "agent-steps/s", "seconds": wall,
+            "executed_agent_steps": agent_steps, "replicas_absorbed": absorbed,
+            "note": "whole run through BatchEngine.run (absorbing stops, group retirement, host syncs, flush)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,6 +169,9 @@ def main():
     ap.add_argument("--replicas", type=int, default=None,
                     help="experiment: first N replicas of the workload grid (cycled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-run", type=int, default=-1,
+                    help="also time the config's whole run (iterations; -1: BASELINE.json's, when it "
+                         "takes under a minute at the measured step time; 0: off)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -160,7 +204,6 @@ def main():
 
     eng.step(W)
     torch.cuda.synchronize()
-    stop_w = eng.stop_iter.cpu().numpy().copy()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -200,9 +243,12 @@ def main():
     per_step_dev_s = dev_ms / 1e3 / K
     step_agents = agent_steps / K
     achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
+    achieved_wall = ALGO_BYTES_PER_AGENT_STEP * agent_steps / wall / 1e9
+    resident, groups, waves = eng.resident, eng.G, eng.waves
+    eng.close()   # before the full run and the CPU baseline's worker processes
 
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "r02", "current", f"traffic_{args.config}.json")
+    tfile = os.path.join(ROOT, "profiles", "r03", f"traffic_{args.config}.json")
     if os.path.exists(tfile) and args.rng == "philox":
         # measured HBM bytes per agent-step (rocprofv3 PMC passes of this same command)
         traffic = json.load(open(tfile))["bytes_per_agent_step"] * step_agents
@@ -214,23 +260,31 @@ def main():
             "data": "synthetic (reference init: S~Bernoulli(1/2), R=0, Q~U(-0.01,0.01))",
             "config": {"workload": desc, "L": L, "replicas_per_gpu": len(reps),
                        "agents_per_gpu": n_agents, "second_order": M2, "state": state,
-                       "rng": args.rng, "streams_per_gpu": eng.resident, "replica_groups": eng.G,
-                       "cache_waves": eng.waves,
+                       "rng": args.rng, "streams_per_gpu": resident, "replica_groups": groups,
+                       "cache_waves": waves,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_unit": "bytes per iteration (all replicas), from profiles/r02/current/traffic_*.json",
+                         "time_base": "HIP events around the K timed iterations (device time per iteration)",
+                         "achieved_wall": achieved_wall, "frac_wall": achieved_wall / HBM_PEAK_GBS,
+                         "traffic_unit": "bytes per iteration (all replicas), from profiles/r03/traffic_*.json",
                          "traffic_gbs": (traffic / per_step_dev_s / 1e9) if traffic else None,
                          "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
-                         "kernel": (f"spgg_step_kernel, {eng.resident} concurrent launches per iteration "
+                         "kernel": (f"spgg_step_kernel, {resident} concurrent launches per iteration "
                                     f"(one per replica group/stream)" if args.rng == "philox" else
-                                    "spgg_mt_draw_kernel + spgg_step_kernel per replica group"),
+                                    f"spgg_step_kernel ({resident} concurrent launches per iteration) + "
+                                    f"spgg_mt_gen_kernel (one launch per 8 iterations per group, on its own "
+                                    f"stream)"),
                          "device_ms_per_step": per_step_dev_s * 1e3},
         }
+        T_full = FULL_RUN_ITERS.get(args.config, 0) if args.full_run < 0 else args.full_run
+        if args.full_run < 0 and wall_max / K * T_full > 60.0:
+            T_full = 0
+        if world == 1 and T_full > 0:
+            line["full_run"] = full_run(L, M2, state, reps, args.rng, args.streams, T_full, 0)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(L, M2, state, reps, args.cpu_budget)
         print(json.dumps(line), flush=True)
-    eng.close()
     if dist:
         dist.destroy_process_group()
 

@@ -18,8 +18,10 @@
  *
  * Conventions: every function returns 0 on success, a negative SPGG_E* code on
  * failure (detail in spgg_last_error).  No C++ exception crosses the ABI.
- * One iteration is ONE kernel launch over all replicas (plus one MT19937 draw
- * launch in that mode; plus one prologue launch before iteration 1).
+ * One iteration is ONE kernel launch over all replicas (plus one prologue launch
+ * before iteration 1).  In MT19937 mode a generator kernel produces the draw
+ * records of 8 iterations per launch (SPGG_MT_CHUNK) on a second stream, one
+ * chunk ahead of the steps (ordered by events; spgg_set_draw_stream).
  * Buffers are DEVICE pointers owned by the caller (e.g. torch tensors); the
  * library only allocates its per-replica parameter table and frees it in
  * spgg_destroy.  A context is bound to one device and is not thread-safe.
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SPGG_ABI_VERSION 10
+#define SPGG_ABI_VERSION 11
 
 #define SPGG_OK 0
 #define SPGG_E_ARG (-1)     /* bad argument / shape */
@@ -166,15 +168,26 @@ typedef struct {
  *                                    feeds is +0 otherwise)
  *   atd       f32    [n_rep][n]      |alpha*td'| of the pending iteration (diagnostic), in place
  *                                    (likewise only for kappa != 0)
- *   draws     uint8  [planes][..][n] the step's random draws as 0/1 bytes (INJECT/MT19937),
- *                                    one plane per draw of the reference, in its order
- *                                    (spgg_draw_planes): plane 2k = (rand < eps) and
- *                                    2k+1 = randint(0,2) of select k (k = 0 the action;
- *                                    SARSA k = 1 next action, k = 2 diagnostic, spgg.py:
- *                                    434,452); Double-Q plane 2 = (rand < 0.5), the table
- *                                    choice (algorithms.py:302).  Replica rep of plane p
- *                                    is at draws + p*draw_plane_stride + rep*n
- *   mt_state  uint32 [n_rep][625]    MT19937 key[624] + pos (MT19937 only)
+ *   draws     uint32 [slots][..][W]  the steps' random draws as BITS (INJECT/MT19937), a ring
+ *                                    of spgg_draw_layout slots: iteration t uses slot
+ *                                    (t-1) % slots at draws + slot*draw_slot_stride, replica
+ *                                    rep at + rep*W (W = words_per_rep).  One plane per draw
+ *                                    of the reference, in its order (spgg_draw_planes): plane
+ *                                    2k = (rand < eps) and 2k+1 = randint(0,2) of select k
+ *                                    (k = 0 the action; SARSA k = 1 next action, k = 2
+ *                                    diagnostic, spgg.py:434,452); Double-Q plane 2 =
+ *                                    (rand < 0.5), the table choice (algorithms.py:307).
+ *                                    Agent g's bit of plane p: bit g % 32 of word
+ *                                    (g / 32) * planes + p (planes interleaved per 32 agents;
+ *                                    W = ceil(n/64) * 2 * planes).  INJECT: the caller writes
+ *                                    slot (t-1) % slots before spgg_step(t); MT19937: the
+ *                                    library's generator fills the ring
+ *   mt_state  uint32 [n_rep][625]    MT19937 key[624] + pos (MT19937 only): the key before the
+ *                                    run; after spgg_flush the key the reference holds after
+ *                                    each replica's last executed iteration
+ *   mt_snap   uint32 [snap_slots][..][625]  key snapshots (MT19937 only; library-internal:
+ *                                    slot t % snap_slots = the key after iteration t),
+ *                                    replica rep at + slot*mt_snap_stride + rep*625
  *   eps       f64    [n_rep][iterations+2]  eps used by iteration t
  *   stats     f64    [n_rep][stripes][iterations+2][SPGG_NSTAT]  zero-initialised;
  *                                    stripe 0 of slot t0 must hold NCOOP of S_t0 before
@@ -192,15 +205,20 @@ typedef struct {
   double* pub[2];
   double* md;
   float* atd;
-  uint8_t* draws;
-  int64_t draw_plane_stride;  /* bytes between draw planes (>= n_rep*n) */
+  uint32_t* draws;
+  int64_t draw_slot_stride;   /* u32 words between draw-record ring slots (>= n_rep*words_per_rep) */
   uint32_t* mt_state;
+  uint32_t* mt_snap;
+  int64_t mt_snap_stride;     /* u32 words between key-snapshot slots (>= n_rep*625) */
   double* eps;
   double* stats;
   int32_t* stop_iter;
 } spgg_buffers;
 
 int spgg_abi_version(void);
+/* Content hash of the sources, compiler flags and defines the library was built from
+ * (build.py): the package refuses an in-tree library whose id differs from the sources. */
+const char* spgg_build_id(void);
 /* Number of draw planes one iteration of `algorithm` consumes: 2, 6 (SARSA), 2, 3 (Double-Q). */
 int spgg_draw_planes(int32_t algorithm);
 /* Detail of the context's last failure; with ctx == NULL, of the calling thread's
@@ -225,6 +243,9 @@ int spgg_step(spgg_ctx* ctx, int32_t t0, int32_t n_steps, void* hip_stream);
 
 /* Apply the deferred neighbor-influence term of iteration t_last (the last
  * executed one) and its Q statistics.  Call once after the final spgg_step.
+ * MT19937: also waits for the generator and restores mt_state to each replica's
+ * key after its last executed iteration (the state np.random holds after the
+ * reference's run).
  * SPGG_E_STATE if a replica's kappa went from 0 to nonzero since the run began
  * (its pending record was never written; see spgg_set_params). */
 int spgg_flush(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
@@ -236,8 +257,18 @@ int spgg_flush(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
  * spgg.py:383-394, 529-545 for those values. */
 int spgg_history_finalize(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
 
-/* Draw the RNG bytes of one iteration only (MT19937 mode; for tests). */
+/* Generate the draw record of iteration t only, from mt_state (advancing it), into its
+ * ring slot (MT19937 mode; for tests -- spgg_step runs the pipelined generator itself). */
 int spgg_draw(spgg_ctx* ctx, int32_t t, void* hip_stream);
+
+/* Draw-record ring of INJECT / MT19937 contexts: ring slots (iterations), u32 words per
+ * replica and slot, and key-snapshot slots (MT19937).  Replaces: the reference's per-step
+ * np.random.rand / randint calls (algorithms.py:105-108) -- their outputs as bits. */
+int spgg_draw_layout(const spgg_ctx* ctx, int32_t* slots, int64_t* words_per_rep, int32_t* snap_slots);
+
+/* MT19937: the stream the draw generator runs on (default: one the library creates per
+ * context).  Contexts of one batch may share one; call before the first spgg_step. */
+int spgg_set_draw_stream(spgg_ctx* ctx, void* hip_stream);
 
 /* P (normalised payoff, spgg.py:373-378) of every agent from S_t into
  * out[n_rep][n] (device).  Used for SPGG.P and run()'s return value. */

@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -31,10 +31,10 @@ ST_GC0, ST_NMD_POS, ST_NMD_POS2, ST_SUM_PCT = 12, 18, 19, 20
 ST_SUMQ, ST_SUMQ_C, ST_SUMQ_D, ST_GMAX = 21, 25, 29, 33
 NSTAT = 34
 
-EXPORTED = ("spgg_abi_version", "spgg_last_error", "spgg_create", "spgg_set_params",
+EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create", "spgg_set_params",
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
-            "spgg_history_finalize")
+            "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream")
 
 
 class Config(ctypes.Structure):
@@ -59,8 +59,9 @@ class RepParams(ctypes.Structure):
 class Buffers(ctypes.Structure):
     _fields_ = [("S", ctypes.c_void_p * 2), ("R", ctypes.c_void_p * 2), ("Q", ctypes.c_void_p),
                 ("pub", ctypes.c_void_p * 2), ("md", ctypes.c_void_p), ("atd", ctypes.c_void_p),
-                ("draws", ctypes.c_void_p),
-                ("draw_plane_stride", ctypes.c_int64), ("mt_state", ctypes.c_void_p), ("eps", ctypes.c_void_p),
+                ("draws", ctypes.c_void_p), ("draw_slot_stride", ctypes.c_int64),
+                ("mt_state", ctypes.c_void_p), ("mt_snap", ctypes.c_void_p), ("mt_snap_stride", ctypes.c_int64),
+                ("eps", ctypes.c_void_p),
                 ("stats", ctypes.c_void_p), ("stop_iter", ctypes.c_void_p)]
 
 
@@ -115,9 +116,22 @@ def load(path: str | None = None):
         lib.spgg_stat_stripes.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
         lib.spgg_pub_doubles.restype = ctypes.c_int
         lib.spgg_pub_doubles.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+        lib.spgg_draw_layout.restype = ctypes.c_int
+        lib.spgg_draw_layout.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32)]
+        lib.spgg_set_draw_stream.restype = ctypes.c_int
+        lib.spgg_set_draw_stream.argtypes = [vp, vp]
+        lib.spgg_build_id.restype = ctypes.c_char_p
+        lib.spgg_build_id.argtypes = []
         v = lib.spgg_abi_version()
         if v != ABI_VERSION:
             raise SpggError(f"libspgg_hip ABI {v} != expected {ABI_VERSION}")
+        if p == LIB_PATH:   # the in-tree library must be built from these sources (a tuning
+            from . import build as B   # build named by path / $SPGG_LIB is the caller's choice)
+            if os.path.exists(B.SRC[0]):
+                want, have = B.build_id(), lib.spgg_build_id().decode()
+                if want != have:
+                    raise SpggError(f"{p} was built from other sources (build id {have}, sources {want}); "
+                                    "rebuild: python -c 'import __graft_entry__ as g; g.build()'")
         _libs[p] = lib
         return lib
 

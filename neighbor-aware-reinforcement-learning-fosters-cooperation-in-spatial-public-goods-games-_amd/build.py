@@ -4,6 +4,7 @@
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -27,18 +28,40 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-munsafe-fp-atomics"]
 
 
-def needs_build(out=OUT):
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    deps = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
+DEPS = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h")]
+
+
+def build_id(defines=()):
+    """16 hex digits of SHA-256 over the sources, compiler, flags and defines: embedded in
+    the library (spgg_build_id(), and as the string "spgg-build:<id>") so that freshness is
+    decided by content, not by file times."""
+    h = hashlib.sha256()
+    for d in DEPS:
+        with open(d, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join([HIPCC, *FLAGS, *sorted(defines)]).encode())
+    return h.hexdigest()[:16]
+
+
+def library_build_id(path):
+    """The build id a built library carries, or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(b"spgg-build:")
+    return data[i + 11:i + 27].decode("ascii", "replace") if i >= 0 else None
+
+
+def needs_build(out=OUT, defines=()):
+    return library_build_id(out) != build_id(defines)
 
 
 def build(force=False, verbose=True, out=OUT, defines=()):
-    if not force and not needs_build(out):
+    if not force and not needs_build(out, defines):
         return out
-    extra = [f"-D{d}" for d in defines]
+    extra = [f"-D{d}" for d in defines] + [f'-DSPGG_BUILD_ID="{build_id(defines)}"']
     with tempfile.TemporaryDirectory() as tmp:
         objs = [os.path.join(tmp, f"tu{k}.o") for k in TUS]
         cmds = [[HIPCC, *FLAGS, *extra, f"-DSPGG_TU={k}", f"-I{INC}", "-c", SRC[0], "-o", o]

@@ -52,20 +52,9 @@ using namespace spgg;
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
-// Pending-NI record per agent (A/B knob): 0 = max_diff (f64) + |alpha*td'| (f32); 1 = a
-// 32-bit pair of reward codes (the agent's and its best neighbour's payoff inputs, from which
-// the next launch recomputes both rewards, max_diff and the diagnostic |alpha*td'| exactly:
-// 16 B less traffic per agent-step, bit-identical, but measured 3 us/step SLOWER on cfg3 --
-// the two payoff recomputes cost more VALU time than the bytes save; profiles/r02/).
-#ifndef SPGG_PEND_CODES
-#define SPGG_PEND_CODES 0
-#endif
-#ifndef SPGG_PRIO
-#define SPGG_PRIO 0  // wave priority while a workgroup issues its loads (0: off)
-#endif
-#ifndef SPGG_PRIO_LATE
-#define SPGG_PRIO_LATE 0  // 1: priority 1 from phase 1b, 2 from phase 2; 2: priority 2 from phase 2
-#endif
+// (Rejected A/B knobs -- reward-code pending records, partial Q stores, non-temporal
+// per-agent streams, wave priorities -- live in profiles/r02/rejected_knobs.patch with
+// their measurements.)
 
 // Build layout: this file is compiled once per RL operator with
 // -DSPGG_TU=<SPGG_ALG_*> (that operator's step kernels only) and once with
@@ -89,8 +78,9 @@ struct TileArgs {
   const double* pub_in;   // border records of iteration t-1 (ring recompute reads them)
   double* pub_out;        // border records of iteration t
   float* atd;             // [rep][n], IN PLACE: |alpha*td'| of iteration t-1 (diagnostic)
-  const uint8_t* draws;   // draw planes (INJECT / MT19937), plane stride `plane`
-  size_t plane;
+  const uint32_t* draws;  // draw record of THIS iteration (INJECT / MT19937): [rep][word][plane] bits
+  int draw_words;         // u32 words per replica (draw_words_of: 32-agent words x planes)
+  int planes;             // draw planes per iteration (draw_planes)
   const double* eps;
   double* stats;          // [rep][stripe][slot][NSTAT]: a workgroup adds to stripe tile % stripes
   int* stop_iter;
@@ -181,12 +171,10 @@ using spgg_impl::TileArgs;
 
 namespace {
 
-constexpr int kMtThreads = 640;  // >= 624 MT19937 words, 10 waves
-
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_Code, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, bytes;
 };
 
 // Pitch of the plus-count plane: one 64-lane wave row per region row.
@@ -212,7 +200,6 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_D = off;    off += ((l.sw * l.sh + kPcPitch + 15) / 16) * 16;  // + slack: full-wave row reads
   l.off_A = off;    off += ((na + 15) / 16) * 16;
   l.off_PC = off;   off += (l.ah + 2) * kPcPitch;
-  l.off_Code = off; off += SPGG_PEND_CODES ? ((na * 2 + 15) / 16) * 16 : 0;
   l.bytes = off;
   return l;
 }
@@ -482,10 +469,10 @@ __device__ __forceinline__ void build_plus_counts_dw(uint8_t* pc, const uint8_t*
 // group defector counts are plus counts at the cell and its four axial
 // neighbours, each a byte offset into tb = the table of the cell's own
 // strategy indexed by defector count; summed in the reference's group order,
-// normalised.  *code: the cell's reward code (pay_code).
+// normalised.
 #define T_AT(t, o) (*reinterpret_cast<const double*>((t) + (o)))
 __device__ __forceinline__ double payoff_pc(const uint8_t* pc, int ry, int rx, const double* tb, double norm_min,
-                                            double norm_den, double norm_rcp, uint32_t* code = nullptr) {
+                                            double norm_den, double norm_rcp) {
   const uint8_t* p = pc + ry * kPcPitch + rx + 1;  // plus count of N0[i-1, j]
   const char* t = reinterpret_cast<const char*>(tb);
   const uint32_t x0 = p[kPcPitch], x1 = p[0], x2 = p[2 * kPcPitch], x3 = p[kPcPitch - 1], x4 = p[kPcPitch + 1];
@@ -494,24 +481,9 @@ __device__ __forceinline__ double payoff_pc(const uint8_t* pc, int ry, int rx, c
   tot = tot + T_AT(t, x2);                     // group (-1,0) -> N0[i+1,j]
   tot = tot + T_AT(t, x3);                     // group (1,1)  -> N0[i,j-1]
   tot = tot + T_AT(t, x4);                     // group (-1,1) -> N0[i,j+1]
-  if (code) *code = (x0 >> 3) | x1 | (x2 << 3) | (x3 << 6) | (x4 << 9);  // x_k = 8 * defector count
   return div_uniform(tot - norm_min, norm_den, norm_rcp);  // (tot - (r-5)) / (4r - (r-5))
 }
 
-// Reward code of an agent: the five group defector counts (3 bits each, bits 0-14,
-// in the reference's group order) and its strategy (bit 15, 1 = D) -- everything its
-// payoff depends on.  pay_code recomputes the payoff from it with payoff_pc's exact
-// operations (same table entries, same order), hence the same double.
-__device__ __forceinline__ double payoff_code(uint32_t code, const double* tab, double norm_min, double norm_den,
-                                              double norm_rcp) {
-  const char* t = reinterpret_cast<const char*>(tab + ((code >> 15) & 1 ? 6 : 0));
-  double tot = T_AT(t, (code & 7) << 3);
-  tot = tot + T_AT(t, code & 0x38);
-  tot = tot + T_AT(t, (code >> 3) & 0x38);
-  tot = tot + T_AT(t, (code >> 6) & 0x38);
-  tot = tot + T_AT(t, (code >> 9) & 0x38);
-  return div_uniform(tot - norm_min, norm_den, norm_rcp);
-}
 #undef T_AT
 
 // 1/x to full f64 precision for DIAGNOSTIC quotients only (history values,
@@ -561,8 +533,15 @@ __device__ __forceinline__ double expected_q(double v0, double v1, double eps) {
 // Draw pair k of agent g at iteration t: explore flag (rand < thr) and the
 // randint bit.  Philox: the agent's half of block (agent pair, t + k*2^26) under the replica key;
 // device MT19937 / inject: planes 2k, 2k+1 of the draw record.
+// Bit g of plane p in this iteration's draw record of replica `rep` (words of 32 agents,
+// the planes of one word interleaved: spgg_abi.h, spgg_buffers.draws).
+__device__ __forceinline__ int draw_bit(const TileArgs& a, int rep, int g, int p) {
+  const uint32_t w = *at(a.draws, (uint32_t)(rep * a.draw_words + (g >> 5) * a.planes + p));
+  return (int)((w >> (g & 31)) & 1u);
+}
+
 template <int RNG>
-__device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, int t, uint32_t key, uint64_t thr,
+__device__ __forceinline__ void draw_pair(const TileArgs& a, int rep, int g, int t, uint32_t key, uint64_t thr,
                                           int k, int* ex, int* rbt) {
   if constexpr (RNG == SPGG_RNG_PHILOX) {
 #if SPGG_ABLATE & 1
@@ -571,49 +550,33 @@ __device__ __forceinline__ void draw_pair(const TileArgs& a, size_t rb, int g, i
     philox_draw(g, t + (k << 26), key, thr, ex, rbt);
 #endif
   } else {
-    *ex = a.draws[(size_t)(2 * k) * a.plane + rb + g];
-    *rbt = a.draws[(size_t)(2 * k + 1) * a.plane + rb + g];
+    *ex = draw_bit(a, rep, g, 2 * k);
+    *rbt = draw_bit(a, rep, g, 2 * k + 1);
   }
 }
 
 // Double-Q's table choice (rand < 0.5, algorithms.py:302): plane 2, or Philox pair 1.
 template <int RNG>
-__device__ __forceinline__ int draw_table1(const TileArgs& a, size_t rb, int g, int t, uint32_t key) {
+__device__ __forceinline__ int draw_table1(const TileArgs& a, int rep, int g, int t, uint32_t key) {
   if constexpr (RNG == SPGG_RNG_PHILOX) {
     int ex, rbt;
     philox_draw(g, t + (1 << 26), key, 1ull << 52, &ex, &rbt);  // rand < 0.5
     return ex;
   } else {
-    return a.draws[(size_t)2 * a.plane + rb + g];
+    return draw_bit(a, rep, g, 2);
   }
 }
 
-// Per-agent streams (Q, md, atd): read once and written once per iteration.
-// SPGG_NT=1 marks them non-temporal (measurement knob: keeps them from
-// displacing the halo windows and border records other tiles re-read in L2).
-#ifndef SPGG_NT
-#define SPGG_NT 0
-#endif
 typedef double vd2 __attribute__((ext_vector_type(2)));
-template <typename T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (SPGG_NT == 1) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <typename T>
-__device__ __forceinline__ void st_stream(T* p, T v) {  // SPGG_NT=2: stores only
-  if constexpr (SPGG_NT != 0) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
 
 template <int QB>
 __device__ __forceinline__ void load_q(const double* Qr, uint32_t agent, double (&q)[4],
                                        double (&qb)[QB ? 4 : 1]) {
   const vd2* qp = at(reinterpret_cast<const vd2*>(Qr), agent * (QB ? 4 : 2));
-  const vd2 q01 = ld_stream(qp), q23 = ld_stream(qp + 1);
+  const vd2 q01 = qp[0], q23 = qp[1];
   q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
   if constexpr (QB) {
-    const vd2 b01 = ld_stream(qp + 2), b23 = ld_stream(qp + 3);
+    const vd2 b01 = qp[2], b23 = qp[3];
     qb[0] = b01.x; qb[1] = b01.y; qb[2] = b23.x; qb[3] = b23.y;
   }
 }
@@ -622,35 +585,11 @@ template <int QB>
 __device__ __forceinline__ void store_q(double* Qr, uint32_t agent, const double (&q)[4],
                                         const double (&qb)[QB ? 4 : 1]) {
   vd2* qo = at(reinterpret_cast<vd2*>(Qr), agent * (QB ? 4 : 2));
-  st_stream(qo, vd2{q[0], q[1]});
-  st_stream(qo + 1, vd2{q[2], q[3]});
+  qo[0] = vd2{q[0], q[1]};
+  qo[1] = vd2{q[2], q[3]};
   if constexpr (QB) {
-    st_stream(qo + 2, vd2{qb[0], qb[1]});
-    st_stream(qo + 3, vd2{qb[2], qb[3]});
-  }
-}
-
-// Stores of the Q entries launch t changed: e_new (TD of t) and e_old (NI term of t-1,
-// -1 if none); every other entry keeps its value in memory.  SPGG_QSTORE: 0 = the whole
-// 32-byte row pair, 1 = the 16-byte rows holding the changed entries, 2 = the 8-byte
-// entries themselves.  Double-Q: whole rows of both tables.
-#ifndef SPGG_QSTORE
-#define SPGG_QSTORE 0
-#endif
-template <int QB>
-__device__ __forceinline__ void store_q_changed(double* Qr, uint32_t agent, const double (&q)[4],
-                                                const double (&qb)[QB ? 4 : 1], int e_new, int e_old) {
-  if constexpr (QB || SPGG_QSTORE == 0) {
-    store_q<QB>(Qr, agent, q, qb);
-  } else if constexpr (SPGG_QSTORE == 1) {
-    vd2* qo = at(reinterpret_cast<vd2*>(Qr), agent * 2);
-    const int rn = e_new >> 1;
-    st_stream(qo + rn, rn ? vd2{q[2], q[3]} : vd2{q[0], q[1]});
-    if (e_old >= 0 && (e_old >> 1) != rn) st_stream(qo + (rn ^ 1), rn ? vd2{q[0], q[1]} : vd2{q[2], q[3]});
-  } else {
-    double* qo = at(Qr, agent * 4);
-    st_stream(qo + e_new, q_get(q, e_new));
-    if (e_old >= 0 && e_old != e_new) st_stream(qo + e_old, q_get(q, e_old));
+    qo[2] = vd2{qb[0], qb[1]};
+    qo[3] = vd2{qb[2], qb[3]};
   }
 }
 
@@ -700,7 +639,7 @@ __device__ __forceinline__ float diag_td_dq(const double (&q)[4], const double (
 // diag = false (kappa == 0: the NI percent it feeds is exactly 0) skips the
 // diagnostic and returns 0.
 template <int ALG, int RNG, typename PT>
-__device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size_t rb, int g, int t,
+__device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, int rep, int g, int t,
                                            uint32_t key, double eps, uint64_t eps53, bool diag, double rew,
                                            int so, int act, int sn, double (&q)[4],
                                            double (&qb)[ALG == ALG_DQ ? 4 : 1], double* rn0, double* rn1) {
@@ -710,7 +649,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     // scalar copies: value selects only (pointer selects into the tables
     // would keep them out of registers)
     double x[4] = {q[0], q[1], q[2], q[3]}, y[4] = {qb[0], qb[1], qb[2], qb[3]};
-    const int up1 = draw_table1<RNG>(a, rb, g, t, key);
+    const int up1 = draw_table1<RNG>(a, rep, g, t, key);
     const double qc1 = q_get(x, e), qc2 = q_get(y, e);
     const double y0 = y[0], y1 = y[1], y2 = y[2], y3 = y[3];
     const double x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
@@ -736,7 +675,7 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
       target = max_f64(v0, v1);                                      // algorithms.py:124-127
     } else if constexpr (ALG == ALG_SARSA) {
       int ex, rbt;                                                   // next action, spgg.py:434
-      draw_pair<RNG>(a, rb, g, t, key, eps53, 1, &ex, &rbt);
+      draw_pair<RNG>(a, rep, g, t, key, eps53, 1, &ex, &rbt);
       target = (ex ? rbt : greedy2(v0, v1)) ? v1 : v0;               // algorithms.py:168-171
     } else {
       target = expected_q(v0, v1, eps);                              // algorithms.py:205-222
@@ -757,29 +696,12 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, size
     double target2;
     if constexpr (ALG == ALG_SARSA) {
       int ex, rbt;                                                   // diagnostic select, spgg.py:452
-      draw_pair<RNG>(a, rb, g, t, key, eps53, 2, &ex, &rbt);
+      draw_pair<RNG>(a, rep, g, t, key, eps53, 2, &ex, &rbt);
       target2 = (ex ? rbt : greedy2(w0, w1)) ? w1 : w0;
     } else {
       target2 = ALG == ALG_ES ? expected_q(w0, w1, eps) : max_f64(w0, w1);
     }
     return (float)fabs(pg.diag_alpha * ((rew + dgamma * target2) - q1));  // Q'[s,a] = q1
-  }
-}
-
-// Diagnostic |diag_alpha*td'| of iteration t-1, recomputed by launch t from the pending
-// record (reward codes): q / qb hold the table after t-1's TD update and before its NI
-// term (the in-place Q between launches), e = (s_old, a), sn = s_t, rew = the agent's
-// reward of t-1 -- td_update's diagnostic operations exactly (spgg.py:446-475).  SARSA's
-// diagnostic needs its own select draw of t-1 (spgg.py:452), so SARSA stores the value.
-template <int ALG, typename PT>
-__device__ __forceinline__ float diag_td_pending(const double (&q)[4], const double (&qb)[ALG == ALG_DQ ? 4 : 1],
-                                                 int e, int sn, double rew, const PT& pg, double eps_prev) {
-  if constexpr (ALG == ALG_DQ) {
-    return diag_td_dq(q, qb, e, sn, rew, pg);
-  } else {
-    const double w0 = sn ? q[2] : q[0], w1 = sn ? q[3] : q[1];
-    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps_prev) : max_f64(w0, w1);
-    return (float)fabs(pg.diag_alpha * ((rew + pg.diag_gamma * target2) - q_get(q, e)));
   }
 }
 
@@ -838,10 +760,6 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   constexpr int QB = ALG == ALG_DQ ? 1 : 0;
   constexpr int QW = QB ? 8 : 4;
   constexpr int PF = spgg_impl::pf_of(ALG);
-  // pending NI record: reward codes (CODES), else max_diff + |alpha*td'|; the
-  // diagnostic is stored (ATD) where it cannot be recomputed from the codes
-  constexpr bool CODES = SPGG_PEND_CODES != 0;
-  constexpr bool ATD = !CODES || ALG == ALG_SARSA;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -872,12 +790,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint8_t* sD = smem + ly.off_D;
   uint8_t* sA = smem + ly.off_A;
   uint8_t* sPC = smem + ly.off_PC;
-  uint16_t* sCode = reinterpret_cast<uint16_t*>(smem + ly.off_Code);  // reward codes (CODES)
   // this replica's arrays: scalar bases, 32-bit element offsets (at())
   const size_t rb = (size_t)rep * n;
   double* Qr = a.Q + rb * QW;
   double* mdr = a.md + rb;
-  uint32_t* pendr = reinterpret_cast<uint32_t*>(a.md) + rb;  // CODES: [rep][n] uint32 in the md buffer
   float* atdr = a.atd + rb;
   const uint8_t* Sin = a.S_in + rb;
   uint8_t* Sout = a.S_out + rb;
@@ -886,7 +802,6 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const bool pending = t > 1;
   const int tid = threadIdx.x;
   const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
-  if (SPGG_PRIO) __builtin_amdgcn_s_setprio(SPGG_PRIO);
   STAMP(0);
 #if SPGG_STAMPS
   if (t == SPGG_STAMP_T && tid == 0 && logical < kStampWG) {
@@ -913,9 +828,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   unsigned vbits = 0;  // bit u: slot u holds an owned agent
   double q[APT][4];
   double qb[APT][QB ? 4 : 1];
-  double md_own[CODES ? 1 : APT];
-  uint32_t pend_own[CODES ? APT : 1];
-  float atd_own[ATD ? APT : 1];
+  double md_own[APT];
+  float atd_own[APT];
   const int n_own = th * tw;
   const uint32_t g00 = (uint32_t)(y0 * L + x0);
   // (row < 256, L < 2^24: a full-rate 24-bit multiply instead of the quarter-rate 32-bit one)
@@ -939,9 +853,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[u][k] = (double)((g + k) & 15) * 1e-3;
         if constexpr (QB) for (int k = 0; k < 4; ++k) qb[u][QB ? k : 0] = q[u][k];
-        if constexpr (CODES) pend_own[u] = g & 0x7fff7fffu;
-        else md_own[u] = 0.0;
-        if constexpr (ATD) atd_own[u] = 0.f;
+        md_own[u] = 0.0;
+        atd_own[u] = 0.f;
       } else {
         load_q<QB>(Qr, g, q[u], qb[u]);
       }
@@ -993,9 +906,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const uint32_t g = ni_rec ? agent_of(rc[u]) : 0u;
-      if constexpr (CODES) pend_own[u] = ld_stream(at(pendr, g));
-      else md_own[u] = ld_stream(at(mdr, g));
-      if constexpr (ATD) atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : ld_stream(at(atdr, g));  // 256: atd traffic floor probe
+      md_own[u] = *at(mdr, g);
+      atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : *at(atdr, g);  // 256: atd traffic floor probe
     }
   }
   // replica state (scalar loads)
@@ -1040,7 +952,6 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
                         (uint32_t)pg.stream_id * 0xC2B2AE35u;
 
-  if (SPGG_PRIO) __builtin_amdgcn_s_setprio(0);
   // windows -> LDS (waits for the loads above)
   if (tid < kParamWords) reinterpret_cast<uint64_t*>(&hps)[tid] = pword;
   else if (tid < kParamWords + 12) reinterpret_cast<uint64_t*>(tab)[tid - kParamWords] = pword;
@@ -1074,9 +985,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
       store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
-      if constexpr (CODES) *at(pendr, agent_of(rc[u])) = pend_own[u];
-      else *at(mdr, agent_of(rc[u])) = md_own[u];
-      if constexpr (ATD) *at(atdr, agent_of(rc[u])) = atd_own[u];
+      *at(mdr, agent_of(rc[u])) = md_own[u];
+      *at(atdr, agent_of(rc[u])) = atd_own[u];
       *at(Sout, agent_of(rc[u])) = sSv[(r + HS) * ly.sw + (c + HS)];
       if (!AS) *at(Rout, agent_of(rc[u])) = sRv[(r + HA) * ly.aw + (c + HA)];
     }
@@ -1097,8 +1007,6 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     float pct = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.0;
-    // eps of iteration t-1 (Expected SARSA's diagnostic target)
-    const double eps_prev = (CODES && ALG == ALG_ES && pending) ? a.eps[(size_t)rep * a.slots + t - 1] : 0.0;
     uint8_t sb[APT];  // S_t bytes of the owned agents: s_t (bit 0) and the state (bit 4) go to rc
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
@@ -1116,25 +1024,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         // U(-0.01,0.01) draws and TD sums of finite values give +0 for exact zeros),
         // and the NI percent is exactly 0
         if (kappa != 0.0) {
-          double mdp;
-          float atdv;
-          if constexpr (CODES) {
-            // both rewards of t-1 from their codes (phase 1b's operations: w_P*P + w_rep*rr),
-            // the best neighbour's action from the match bit; max(0, max_diff) as phase 2
-            const uint32_t pc2 = pend_own[u];
-            const int act = b & 1, an = ((b >> 2) & 1) ? act : act ^ 1;
-            const double rs = w_p * payoff_code(pc2 & 0xffffu, tab, hp.norm_min, hp.norm_den, hp.norm_rcp) +
-                              w_rep * (act == 0 ? 0.5 : 0.0);
-            const double rn = w_p * payoff_code(pc2 >> 16, tab, hp.norm_min, hp.norm_den, hp.norm_rcp) +
-                              w_rep * (an == 0 ? 0.5 : 0.0);
-            const double md = rn - rs;
-            mdp = md > 0.0 ? md : 0.0;
-            if constexpr (ATD) atdv = atd_own[u];
-            else atdv = diag_td_pending<ALG>(q[u], qb[u], e, (b >> 4) & 1, rs, hp, eps_prev);
-          } else {
-            mdp = md_own[u];
-            atdv = atd_own[u];
-          }
+          const double mdp = md_own[u];
+          const float atdv = atd_own[u];
           const double nu = pending_nu(b, mdp, kappa, lam_den, lam_rcp);
           // Q[s,a] += nu as exact masked FMAs: fma(1, nu, x) = x + nu, fma(0, nu, x) = x
 #pragma unroll
@@ -1176,7 +1067,6 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
   }
   STAMP(2);
-  if (SPGG_PRIO_LATE == 1) __builtin_amdgcn_s_setprio(1);
   __syncthreads();  // plus counts and ring records complete
 
   // ---- phase 1b: iteration start + action select for owned agents --------
@@ -1207,10 +1097,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int cs = (r + HS) * ly.sw + (c + HS);
       const int ca = (r + HA) * ly.aw + (c + HA);
       const int s_t = (rc[u] >> 3) & 1;                     // (S_t bits, recorded in phase 1a)
-      uint32_t code;
       const double P = payoff_pc(sPC, r + HA, c + HA, tab + (s_t ? 6 : 0), hp.norm_min, hp.norm_den,
-                                 hp.norm_rcp, &code);
-      if (CODES && acting) sCode[ca] = (uint16_t)(code | (s_t << 15));
+                                 hp.norm_rcp);
       const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sRv[ca];
       if constexpr (RQ) rsum += one ? r_t : 0;             // spgg.py:394 (units)
       else rsum = __builtin_fma(r_t, vmu, rsum);
@@ -1230,7 +1118,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                                                             // R_t (S_t bit 4; iteration 1: the prologue)
       int ex, rbt;                                          // algorithms.py:105-109
       if constexpr (PAIRED) philox_decide(pbits[u], eps53, &ex, &rbt);
-      else draw_pair<RNG>(a, rb, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
+      else draw_pair<RNG>(a, rep, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
       double qs0, qs1;
       select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
       const int act = ex ? rbt : greedy2(qs0, qs1);         // argmax ties -> 0
@@ -1288,12 +1176,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
           }
         }
       }
-      uint32_t code;
-      const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp,
-                                 &code);
+      const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp);
       const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sRv[ay * ly.aw + ax]);
       int ex, rbt;
-      draw_pair<RNG>(a, rb, g, t, pkey, eps53, 0, &ex, &rbt);
+      draw_pair<RNG>(a, rep, g, t, pkey, eps53, 0, &ex, &rbt);
       const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
       const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
       const double rr = act == 0 ? 0.5 : 0.0;
@@ -1302,12 +1188,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       sA[ca] = (uint8_t)act;
       sRn[ca] = (RT)rn;
       sRew[ca] = wpp + wrr;
-      if constexpr (CODES) sCode[ca] = (uint16_t)(code | ((b & 1u) << 15));
     }
   }
   __syncthreads();
   STAMP(4);
-  if (SPGG_PRIO_LATE) __builtin_amdgcn_s_setprio(2);
 
   // ---- phase 2: learn for owned agents -----------------------------------
   double bmax = 0.0;
@@ -1323,7 +1207,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     // the stored diagnostic |alpha*td'| (kappa == 0: the NI percent it feeds is exactly 0), as a
     // scalar flag (an f64 compare has no scalar form and was repeated on the VALU per agent)
     const bool ni_on = __builtin_amdgcn_readfirstlane((int)(kappa != 0.0)) != 0;
-    const bool diag_on = ATD && ni_on;
+    const bool diag_on = ni_on;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
@@ -1334,16 +1218,11 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       int sn;                                               // spgg.py:423
       if constexpr (AS) sn = act == 0 ? 1 : 0;
       else sn = rep_state_lds<M2>(sRn, ca, ly.aw);
-      // (the diagnostic only where it is stored; with reward codes the next launch recomputes it)
       double rn0, rn1;  // row s_{t+1} of the updated table (the border record's)
-      const float atd = td_update<ALG, RNG>(a, hp, rb, agent_of(rc[u]), t, pkey, eps_t, eps53, diag_on, rew, so,
+      const float atd = td_update<ALG, RNG>(a, hp, rep, agent_of(rc[u]), t, pkey, eps_t, eps53, diag_on, rew, so,
                                             act, sn, q[u], qb[u], &rn0, &rn1);
-      if (diag_on && !(SPGG_ABLATE & (256 | 2048))) st_stream(at(atdr, agent_of(rc[u])), atd);  // read only for the NI percent (0 when kappa == 0)
-      if (!(SPGG_ABLATE & 2048)) {
-        // entry the NI term of t-1 changed in phase 1a (none at t = 1 or with kappa == 0)
-        const int e_old = (pending && kappa != 0.0) ? pending_entry(sSv[(r + HS) * ly.sw + (c + HS)]) : -1;
-        store_q_changed<QB>(Qr, agent_of(rc[u]), q[u], qb[u], so * 2 + act, e_old);
-      }
+      if (diag_on && !(SPGG_ABLATE & (256 | 2048))) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
+      if (!(SPGG_ABLATE & 2048)) store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);  // the whole row pair
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -1362,27 +1241,20 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       }
       double md = rw[0] - rew;
       int abest = an[0], ks = 0;      // best neighbour's action (and offset index, M=2)
-      int cbest = nb[0];              // best neighbour's region cell (its reward code)
 #pragma unroll
       for (int kk = 1; kk < KN; ++kk) {
         const double d = rw[kk] - rew;
         const bool better = d > md;
         md = max_f64(md, d);  // = better ? d : md (equal values are equal doubles: rewards are never -0)
         abest = better ? an[kk] : abest;
-        if constexpr (CODES) cbest = better ? nb[kk] : cbest;
         if constexpr (M2) ks = better ? kk : ks;
       }
       const int dp = abest == act ? 1 : 0;
       const double mdp = md > 0.0 ? md : 0.0;
       bmax = max_f64(bmax, mdp);
-      if (SPGG_ABLATE & 2048) {
-      } else if constexpr (CODES) {
-        st_stream(at(pendr, agent_of(rc[u])), (uint32_t)sCode[ca] | ((uint32_t)sCode[cbest] << 16));
-      } else {
-        // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
-        // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)
-        if (ni_on) st_stream(at(mdr, agent_of(rc[u])), mdp);
-      }
+      // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
+      // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)
+      if (ni_on && !(SPGG_ABLATE & 2048)) *at(mdr, agent_of(rc[u])) = mdp;
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
       const int bslot = (int)(int16_t)(uint16_t)(bsw >> (16 * u));  // (table: border_slot_table)
@@ -1653,10 +1525,32 @@ namespace {
 
 // ---------------------------------------------------------------------------
 // Device MT19937, bit-identical to numpy.random.RandomState (legacy seeding,
-// randomkit mt19937_gen + tempering).  One workgroup per replica owns its
-// 624-word key in LDS; the twist runs in three dependency phases.
+// randomkit mt19937_gen + tempering), generating the draw records of whole
+// chunks of iterations ahead of the step kernels (spgg_step runs it on its own
+// stream; the draws depend on nothing but the key and the eps schedule).
+//
+// The raw word stream obeys x[k+624] = x[k+397] ^ twist(x[k], x[k+1]), so the 227
+// words of a block [F, F+227) depend only on words >= 227 back: block-parallel.
+// One workgroup per replica, no barrier after the prologue:
+//   waves 0..kGenNR-1, the recurrence: the 227 positions of a block in 4 slots of lanes, two
+//     per wave (gen_slot_base), x[F+j] from x[F+j-227] (the lane's previous word of the
+//     slot, a register) and x[F+j-624], x[F+j-623] (the LDS ring, 2-3 blocks old; read one
+//     block ahead).  Each wave publishes its completed blocks (gen_done) and reads another
+//     wave's words only from blocks >= 2 behind; one wave's LDS operations complete in
+//     order.  The ring holds kGenNB blocks at fixed positions (block b at 256*(b % kGenNB),
+//     + a mirror of block 0 behind the last one), so with the block loop unrolled kGenNB
+//     times every LDS address is a lane constant plus an immediate offset, and no LDS
+//     operation of the recurrence sits under a branch;
+//   the other kGenOut waves: temper + threshold + pack the finished words (below the
+//     frontier 624 + 227*min(gen_done)): 64 draws per wave instruction, one __ballot, two
+//     32-bit stores -- the draw record holds one BIT per draw (spgg_abi.h).  They publish
+//     the first word they still need (gen_need), which the recurrence must not overwrite.
 // Per executed iteration the reference draws rand(L,L) (2 words per double,
-// algorithms.py:105) then randint(0,2,(L,L)) (1 word each, algorithms.py:108).
+// algorithms.py:105) then randint(0,2,(L,L)) (1 word each, algorithms.py:108);
+// SARSA twice more (spgg.py:434, 452), Double-Q then rand(L,L) < 0.5
+// (algorithms.py:307).  After each iteration the key (the 624-word block holding
+// the last consumed word, + pos) is saved to a snapshot ring, from which
+// spgg_flush restores the key the reference would hold (spgg_mt_final_kernel).
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
@@ -1665,92 +1559,295 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-__device__ __forceinline__ uint32_t mt_mix(uint32_t hi, uint32_t lo, uint32_t far) {
-  const uint32_t y = (hi & 0x80000000u) | (lo & 0x7fffffffu);
-  return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+// x[k+624] = x[k+397] ^ twist(x[k], x[k+1]): upper bit of x[k], lower 31 of x[k+1]
+__device__ __forceinline__ uint32_t mt_next(uint32_t far, uint32_t lo_k, uint32_t lo_k1) {
+  const uint32_t y = (lo_k & 0x80000000u) | (lo_k1 & 0x7fffffffu);
+  return far ^ (y >> 1) ^ ((lo_k1 & 1u) ? 0x9908b0dfu : 0u);
 }
 
-__device__ void mt_twist(uint32_t* mt) {
-  const int i = threadIdx.x;
-  uint32_t o_i = 0, o_i1 = 0, o_far = 0;
-  if (i < 624) {
-    o_i = mt[i];
-    if (i < 623) o_i1 = mt[i + 1];
-    if (i < 227) o_far = mt[i + 397];
-  }
-  __syncthreads();
-  if (i < 227) mt[i] = mt_mix(o_i, o_i1, o_far);
-  __syncthreads();
-  if (i >= 227 && i < 454) mt[i] = mt_mix(o_i, o_i1, mt[i - 227]);
-  __syncthreads();
-  if (i >= 454 && i < 624) mt[i] = mt_mix(o_i, (i == 623) ? mt[0] : o_i1, mt[i - 227]);
-  __syncthreads();
-}
-
-// Draw program of one iteration, in the reference's order: a segment is
-// rand(L,L) compared with a threshold (2 words per value, "D") or
-// randint(0,2,(L,L)) (1 word, "I"); segment i fills draw plane i.
+// Draw program of one iteration, in the reference's order: plane i is rand(L,L)
+// compared with a threshold (2 words per value, i even) or randint(0,2,(L,L))
+// (1 word, i odd).
 //   Q-learning / Expected SARSA: D(eps) I            (algorithms.py:105,108)
 //   SARSA:   D(eps) I D(eps) I D(eps) I              (+ spgg.py:434, 452)
-//   Double-Q: D(eps) I D(0.5)                        (+ algorithms.py:302)
+//   Double-Q: D(eps) I D(0.5)                        (+ algorithms.py:307)
 __host__ __device__ inline int draw_planes(int alg) {
   return alg == SPGG_ALG_SARSA ? 6 : alg == SPGG_ALG_DOUBLE_Q ? 3 : 2;
 }
+// MT words one iteration consumes, and the first word of plane p within them.
+__host__ __device__ inline int64_t draw_mt_words(int64_t n, int planes) { return n * (planes / 2 * 3 + (planes & 1) * 2); }
+__host__ __device__ inline uint32_t plane_word0(uint32_t n, int p) { return n * (uint32_t)(p / 2 * 3 + (p & 1) * 2); }
+// u32 words of one replica's draw record: 64-draw chunks (two words each) x planes.
+__host__ __device__ inline int64_t draw_words_of(int n, int alg) {
+  return (int64_t)((n + 63) / 64) * 2 * draw_planes(alg);
+}
 
-__global__ __launch_bounds__(kMtThreads) void spgg_mt_draw_kernel(
-    uint32_t* mt_state, uint8_t* draws, size_t plane, const double* eps, const double* stats,
-    const int* stop_iter, int n, int slots, int t, int alg, int stripes) {
-  __shared__ uint32_t mt[624];
-  __shared__ uint32_t carry;
-  const int rep = blockIdx.x;
-  const int st = stop_iter[rep];
-  if (st != 0 && st < t) return;
-  double nc = 0.0;  // NCOOP of S_t: the sum over the replica's record stripes
-  for (int k = 0; k < stripes; ++k) nc += stats[(((size_t)rep * stripes + k) * slots + t) * SPGG_NSTAT + SPGG_ST_NCOOP];
-  if (nc == 0.0 || nc == (double)n) return;  // absorbing: no draw this iteration
-  uint32_t* gstate = mt_state + (size_t)rep * 625;
-  const int tid = threadIdx.x;
-  if (tid < 624) mt[tid] = gstate[tid];
-  int pos = (int)gstate[624];
-  __syncthreads();
-  const double e = eps[(size_t)rep * slots + t];
-  const int nseg = draw_planes(alg);
-  long long seg_start[7];
-  seg_start[0] = 0;
-  for (int i = 0; i < nseg; ++i) seg_start[i + 1] = seg_start[i] + ((i & 1) ? (long long)n : 2LL * n);
-  const long long total = seg_start[nseg];
-  long long produced = 0;
-  while (produced < total) {
-    if (pos == 624) {
-      mt_twist(mt);
-      pos = 0;
-    }
-    const int avail = (int)min((long long)(624 - pos), total - produced);
-    if (tid >= pos && tid < pos + avail) {
-      const long long w = produced + (tid - pos);
-      int sg = 0;
-      while (w >= seg_start[sg + 1]) ++sg;
-      const long long v = w - seg_start[sg];
-      uint8_t* out = draws + (size_t)sg * plane + (size_t)rep * n;
-      const uint32_t y = mt_temper(mt[tid]);
-      if ((sg & 1) == 0) {
-        const double thr = (alg == SPGG_ALG_DOUBLE_Q && sg == 2) ? 0.5 : e;
-        if ((v & 1) == 0) {
-          if (tid + 1 < pos + avail) out[v >> 1] = mt_double(y, mt_temper(mt[tid + 1])) < thr ? 1 : 0;
-          else carry = y;  // pair straddles the key block
-        } else if (tid == pos) {
-          out[v >> 1] = mt_double(carry, y) < thr ? 1 : 0;
-        }
-      } else {
-        out[v] = (uint8_t)(y & 1u);
-      }
-    }
-    produced += avail;
-    pos += avail;
-    __syncthreads();
+#ifndef SPGG_GEN_OUT
+#define SPGG_GEN_OUT 7
+#endif
+// Timing-only generator ablations (-DSPGG_GEN_ABLATE=mask; draws are WRONG): 1 = no output
+// work (the output waves only track the frontier), 2 = no recurrence arithmetic
+#ifndef SPGG_GEN_ABLATE
+#define SPGG_GEN_ABLATE 0
+#endif
+#ifndef SPGG_GEN_NR
+#define SPGG_GEN_NR 2
+#endif
+constexpr int kGenOut = SPGG_GEN_OUT;            // output waves
+constexpr int kGenNR = SPGG_GEN_NR;              // recurrence waves (1 or 2)
+static_assert(kGenNR == 1 || kGenNR == 2, "recurrence waves: 1 or 2");
+constexpr int kGenSPW = 4 / kGenNR;              // slots per recurrence wave
+constexpr int kGenThreads = 64 * (kGenNR + kGenOut);
+constexpr int kMtBlock = 227;                    // 624 - 397: words one dependency step produces
+constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
+constexpr int kGenNB = 16;                       // ring blocks
+constexpr int kGenRing = kGenPitch * (kGenNB + 1);  // + a mirror of block 0 behind the last one
+// Bound of every wait loop between the generator's waves (~0.5 s of s_sleep): a wait that
+// long means a defect, and the kernel then ends with wrong draws instead of hanging the GPU
+constexpr uint32_t kGenSpinMax = 1u << 23;
+
+// The 227 positions of a block in 4 slots of 64 lanes: slot s holds positions
+// base(s) + lane for lane < len(s).  Positions 169-226 need positions 0-57 of the block two
+// back (every other position only blocks three back), so slots 0 and 1 -- the same wave --
+// hold both: a wave reads another wave's words only from blocks >= 2 behind, which leaves
+// each wave a block of slack.  The lanes past len(s) (29 = 256 - 227 of them) own the
+// padding positions 227-255, so every LDS write is unconditional.
+__host__ __device__ constexpr int gen_slot_base(int s) { return s == 0 ? 0 : s == 1 ? 169 : s == 2 ? 58 : 122; }
+__host__ __device__ constexpr int gen_slot_len(int s) { return s == 0 ? 58 : s == 1 ? 58 : s == 2 ? 64 : 47; }
+__host__ __device__ constexpr int gen_slot_pad(int s) { return s == 0 ? 227 : s == 1 ? 233 : s == 2 ? 239 : 239 - 47; }
+__device__ __forceinline__ int gen_position(int s, int lane) {
+  return lane < gen_slot_len(s) ? gen_slot_base(s) + lane : gen_slot_pad(s) + lane - gen_slot_len(s);
+}
+// Ring position of block-relative offset o (< 454) of ring block B: a spill past 227 is the
+// next block's start, 29 words further (block kGenNB lands on the mirror of block 0).
+__device__ __forceinline__ uint32_t gen_spill(uint32_t o) { return o + (o >= (uint32_t)kMtBlock ? kGenPitch - kMtBlock : 0u); }
+
+struct GenArgs {
+  uint32_t* mt_state;      // [rep][625] running key + pos
+  uint32_t* snap;          // snapshot slot s of replica rep: snap + s*snap_stride + rep*625
+  int64_t snap_stride;
+  int snap_slots;
+  uint32_t* draws;         // draw record of iteration t: draws + ((t-1) % draw_slots)*draw_stride
+  int64_t draw_stride;
+  int draw_slots;
+  int draw_words;          // per replica (draw_words_of)
+  const double* eps;       // [rep][eps_slots]
+  int eps_slots;
+  const int* stop_iter;
+  int n, alg;
+};
+
+// Flags shared through LDS between the generator's waves: relaxed workgroup-scope atomics
+// on the __shared__ array itself (plain ds_read / ds_write; through a generic pointer they
+// become flat accesses with system-scope waits).  Every lane of a wave writes its own copy
+// (no branch around the store, so the wait counters stay exact); readers read lane 0's.  A
+// store is placed after every earlier LDS write of the wave (compiler barrier); one wave's
+// LDS operations complete in issue order, so a wave that reads the flag sees those writes.
+#define LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define LDS_ST(x, v)                                                          \
+  do {                                                                        \
+    asm volatile("" ::: "memory");                                            \
+    __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+  } while (0)
+
+// Word k of a launch (the key block = words 0..623) lives in ring block (k + 57) / 227 - 3
+// (mod kGenNB), at offset (k + 57) % 227: blocks b >= 0 hold words 624 + 227 b ..
+__device__ __forceinline__ uint32_t gen_word_pos(uint32_t k) {
+  const uint32_t kk = k + 57, B = kk / kMtBlock;
+  return (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB) + (kk - B * kMtBlock);
+}
+
+// Iterations t0..t1 of every replica (blockIdx.x), from the key in mt_state; writes the
+// draw records, the key snapshots (slot t % snap_slots = the key after iteration t;
+// t0 == 1 also slot 0 = the initial key) and the advanced key.  Word indices are
+// absolute within the launch (the host keeps a launch below 2^31 words: gen_chunk).
+// skip_stopped: replicas already absorbed are left alone (their draws are never read).
+__global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int t0, int t1, int skip_stopped) {
+  __shared__ uint32_t ring[kGenRing];
+  __shared__ uint32_t gen_done[kGenNR][64];   // blocks recurrence wave r has completed (per lane)
+  __shared__ uint32_t gen_need[kGenOut][64];  // output wave w reads no word below this (per lane)
+  const int rep = blockIdx.x, tid = threadIdx.x;
+  if (skip_stopped && g.stop_iter[rep] != 0) return;
+  uint32_t* key = g.mt_state + (size_t)rep * 625;
+  for (int i = tid; i < 624; i += kGenThreads) ring[gen_word_pos(i)] = key[i];
+  if (tid < 64 * kGenNR) gen_done[tid >> 6][tid & 63] = 0;
+  if (tid < 64 * kGenOut) gen_need[tid >> 6][tid & 63] = 0;
+  if (t0 == 1) {
+    uint32_t* s0 = g.snap + (size_t)rep * 625;
+    for (int i = tid; i < 625; i += kGenThreads) s0[i] = key[i];
   }
-  if (tid < 624) gstate[tid] = mt[tid];
-  if (tid == 0) gstate[624] = (uint32_t)pos;
+  const uint32_t pos0 = key[624];  // next word to consume (624: the block is exhausted)
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int planes = draw_planes(g.alg);
+  const uint32_t W = (uint32_t)draw_mt_words(g.n, planes);
+  // blocks of 227 words this launch generates: through the key block of its last iteration
+  uint32_t nblk;
+  {
+    const uint32_t E_last = pos0 + (uint32_t)(t1 - t0 + 1) * W;
+    const uint32_t target_last = ((E_last - 1) / 624) * 624 + 624;
+    nblk = target_last > 624 ? (target_last - 624 + kMtBlock - 1) / kMtBlock : 0;
+  }
+  if (wave < kGenNR) {
+    // ---- the recurrence: wave r owns slots [r*kGenSPW, (r+1)*kGenSPW) of every block ------
+    __builtin_amdgcn_s_setprio(3);  // the critical path
+    const int r = wave;
+    uint32_t prev[kGenSPW], ca[kGenSPW], cb[kGenSPW];
+    uint32_t *wp[kGenSPW], *pa[kGenSPW], *pb[kGenSPW];  // lane addresses: own word, its two operands
+#pragma unroll
+    for (int i = 0; i < kGenSPW; ++i) {
+      const int j = gen_position(r * kGenSPW + i, lane);
+      wp[i] = ring + j;
+      pa[i] = ring + gen_spill(j + 57);
+      pb[i] = ring + gen_spill(j + 58);
+      prev[i] = wp[i][(kGenNB - 1) * kGenPitch];  // x[397 + j]: block -1
+      ca[i] = pa[i][(kGenNB - 3) * kGenPitch];    // operands of block 0: block -3
+      cb[i] = pb[i][(kGenNB - 3) * kGenPitch];
+    }
+    uint32_t E = pos0 + W;
+    uint32_t mb = ((E - 1) / 624) * 624, target = mb + 624;
+    uint32_t lim = 0;   // largest F whose block may be written (output waves' reads)
+    uint32_t mind = 0;  // blocks every recurrence wave has completed (as last read)
+    int t = t0;
+    uint32_t key_mb = 0, key_pos = pos0;
+    uint32_t b = 0;     // blocks this wave has completed
+    // key after iteration t (words [mb, mb+624) and pos), to the snapshot ring; then the next
+    auto retire = [&]() {
+      uint32_t* sn = g.snap + (size_t)(t % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
+#pragma unroll
+      for (int m = 0; m < 10; ++m) {
+        const uint32_t i = lane + 64 * m;
+        if (i < 624) sn[i] = ring[gen_word_pos(mb + i)];
+      }
+      if (lane == 0) sn[624] = E - mb;
+      key_mb = mb;
+      key_pos = E - mb;
+      ++t;
+      E += W;
+      mb = ((E - 1) / 624) * 624;
+      target = mb + 624;
+    };
+    auto poll_done = [&]() {  // min over the recurrence waves' completed blocks
+      uint32_t m = LDS_LD(gen_done[0][0]);
+      if constexpr (kGenNR > 1) m = min(m, LDS_LD(gen_done[1][0]));
+      return __builtin_amdgcn_readfirstlane(m);
+    };
+    // one block: b % kGenNB == U; operands ca/cb were read one block ahead
+#define SPGG_GEN_BLOCK(U)                                                                                 \
+  {                                                                                                       \
+    if (b == nblk) goto rec_done;                                                                         \
+    /* the other wave's blocks <= b-2, read by the prefetch below (block b+1's operands) */               \
+    for (uint32_t spin = 0; kGenNR > 1 && mind + 1 < b && spin < kGenSpinMax; ++spin) {                   \
+      mind = poll_done();                                                                                 \
+      if (mind + 1 < b) __builtin_amdgcn_s_sleep(1);                                                      \
+    }                                                                                                     \
+    if (r == 0)                                                                                           \
+      while (t <= t1 && 624u + kMtBlock * mind >= target) retire();                                       \
+    const uint32_t F = 624u + kMtBlock * b;                                                               \
+    for (uint32_t spin = 0; F > lim && spin < kGenSpinMax; ++spin) { /* flow control: no output wave      \
+                                                            still reads the positions written */          \
+      uint32_t m = 0xffffffffu;                                                                           \
+      _Pragma("unroll") for (int w = 0; w < kGenOut; ++w) m = min(m, LDS_LD(gen_need[w][0]));             \
+      m = __builtin_amdgcn_readfirstlane(m);                                                              \
+      /* (saturating: finished output waves publish 0xffffffff) */                                       \
+      lim = m > 0xffffffffu - (kGenNB - 1) * kMtBlock ? 0xffffffffu : m + (kGenNB - 1) * kMtBlock;        \
+      if (F > lim) __builtin_amdgcn_s_sleep(2);                                                           \
+    }                                                                                                     \
+    uint32_t na[kGenSPW], nb[kGenSPW];                                                                    \
+    _Pragma("unroll") for (int i = 0; i < kGenSPW; ++i) {                                                 \
+      constexpr int rb = ((U + 1 + kGenNB - 3) % kGenNB) * kGenPitch;                                     \
+      na[i] = pa[i][rb];                                                                                  \
+      nb[i] = pb[i][rb];                                                                                  \
+    }                                                                                                     \
+    _Pragma("unroll") for (int i = 0; i < kGenSPW; ++i) {                                                 \
+      const uint32_t x = (SPGG_GEN_ABLATE & 2) ? prev[i] ^ ca[i] : mt_next(prev[i], ca[i], cb[i]);        \
+      prev[i] = x;                                                                                        \
+      wp[i][U * kGenPitch] = x;                                                                           \
+      if (U == 0) wp[i][kGenNB * kGenPitch] = x; /* mirror of block 0 */                                  \
+      ca[i] = na[i];                                                                                      \
+      cb[i] = nb[i];                                                                                      \
+    }                                                                                                     \
+    ++b;                                                                                                  \
+    LDS_ST(gen_done[r][lane], b);                                                                         \
+    if constexpr (kGenNR > 1) mind = poll_done(); /* used by the next block */                            \
+    else mind = b;                                                                                        \
+  }
+    static_assert(kGenNB == 16, "the block loop below is unrolled kGenNB times");
+    for (;;) {
+      SPGG_GEN_BLOCK(0) SPGG_GEN_BLOCK(1) SPGG_GEN_BLOCK(2) SPGG_GEN_BLOCK(3)
+      SPGG_GEN_BLOCK(4) SPGG_GEN_BLOCK(5) SPGG_GEN_BLOCK(6) SPGG_GEN_BLOCK(7)
+      SPGG_GEN_BLOCK(8) SPGG_GEN_BLOCK(9) SPGG_GEN_BLOCK(10) SPGG_GEN_BLOCK(11)
+      SPGG_GEN_BLOCK(12) SPGG_GEN_BLOCK(13) SPGG_GEN_BLOCK(14) SPGG_GEN_BLOCK(15)
+    }
+#undef SPGG_GEN_BLOCK
+  rec_done:
+    if (r != 0) return;
+    for (uint32_t spin = 0; mind < nblk && spin < kGenSpinMax; ++spin) {  // every wave's last block
+      mind = poll_done();
+      if (mind < nblk) __builtin_amdgcn_s_sleep(1);
+    }
+    while (t <= t1) retire();  // (the frontier covers every remaining target)
+    for (int i = lane; i < 624; i += 64) key[i] = ring[gen_word_pos(key_mb + i)];
+    if (lane == 0) key[624] = key_pos;
+    return;
+  }
+  // ---- output waves: chunks ow, ow + kGenOut, ... of each iteration, plane-major --------
+  const int ow = wave - kGenNR;
+  const uint64_t thr_half = u53_threshold(0.5);
+  const int nchunk = (g.n + 63) / 64;
+  uint32_t kpos = pos0;
+  uint32_t seen = 624;  // the frontier as last read
+  for (int t = t0; t <= t1; ++t) {
+    const uint64_t thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t]);
+    uint32_t* rec_out = g.draws + (size_t)((t - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
+    int p = 0, c = ow;
+    while (p < planes && c >= nchunk) { c -= nchunk; ++p; }
+    while (p < planes) {
+      const uint32_t base = kpos + plane_word0((uint32_t)g.n, p);
+      const int cnt = min(64, g.n - 64 * c);
+      const bool dbl = (p & 1) == 0;
+      const uint32_t first = base + (dbl ? 128u : 64u) * (uint32_t)c;
+      const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
+      LDS_ST(gen_need[ow][lane], first);
+      for (uint32_t spin = 0; seen <= last && spin < kGenSpinMax; ++spin) {  // wait for the recurrence
+        uint32_t m = LDS_LD(gen_done[0][0]);
+        if constexpr (kGenNR > 1) m = min(m, LDS_LD(gen_done[1][0]));
+        seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(m);
+        if (seen <= last) __builtin_amdgcn_s_sleep(1);
+      }
+      if (!(SPGG_GEN_ABLATE & 1)) {
+        // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
+        const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
+        const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
+        bool flag;
+        if (dbl) {  // rand() < thr: ((a>>5) * 2^26 + (b>>6)) / 2^53 < thr as a 53-bit integer compare
+          const uint32_t o = o0 + 2 * lane;
+          const uint32_t a = mt_temper(rb[gen_spill(o)]), b = mt_temper(rb[gen_spill(o + 1)]);
+          const uint64_t v = ((uint64_t)(a >> 5) << 26) | (b >> 6);
+          flag = v < ((g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr);
+        } else {    // randint(0, 2) = the word's low bit
+          flag = (mt_temper(rb[gen_spill(o0 + lane)]) & 1u) != 0;
+        }
+        const uint64_t bits = __ballot(flag && lane < cnt);  // (lanes past n read stale words)
+        if (lane < 2) rec_out[(2 * c + lane) * planes + p] = (uint32_t)(lane ? bits >> 32 : bits);
+      }
+      c += kGenOut;
+      while (p < planes && c >= nchunk) { c -= nchunk; ++p; }
+    }
+    kpos += W;
+  }
+  LDS_ST(gen_need[ow][lane], 0xffffffffu);  // done: never blocks the recurrence
+}
+
+// spgg_flush (MT19937): the key the reference holds after the run -- after the last
+// iteration a replica executed (its absorbing iteration draws nothing) -- from the ring.
+__global__ void spgg_mt_final_kernel(GenArgs g, int t_last) {
+  const int rep = blockIdx.x;
+  const int st = g.stop_iter[rep];
+  const int src = st ? st - 1 : t_last;
+  const uint32_t* sn = g.snap + (size_t)(src % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
+  uint32_t* key = g.mt_state + (size_t)rep * 625;
+  for (int i = threadIdx.x; i < 625; i += blockDim.x) key[i] = sn[i];
 }
 
 // History values derived from device counts (spgg_history_finalize), for iterations
@@ -1838,6 +1935,15 @@ struct spgg_ctx {
   spgg_buffers buf{};
   bool bound = false;
   bool params_set = false;
+  // MT19937 draw pipeline: the generator runs gen_chunk iterations per launch on its own
+  // stream, one chunk ahead of the steps; draw records in a ring of draw_slots = 2 chunks,
+  // key snapshots in a ring of snap_slots (spgg_draw_layout)
+  int gen_chunk = 8, draw_slots = 16, snap_slots = 25;
+  int64_t draw_words = 0;            // u32 words of one replica's draw record
+  hipStream_t gen_stream = nullptr;  // the generator's stream (library-owned unless set)
+  bool own_gen_stream = false;
+  hipEvent_t gen_done[2] = {nullptr, nullptr}, step_done[2] = {nullptr, nullptr}, gen_idle = nullptr;
+  int gen_upto = 0;                  // iterations whose generation is enqueued
   std::vector<double> kappa_host;  // the replicas' kappa as last set
   bool kappa_woke = false;         // a kappa went 0 -> nonzero since the run's iteration 1
   spgg_rep_params* d_params = nullptr;
@@ -1986,8 +2092,11 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   a.Q = c->buf.Q;
   a.md = c->buf.md;
   a.atd = c->buf.atd;
-  a.draws = c->buf.draws;
-  a.plane = (size_t)c->buf.draw_plane_stride;
+  // this iteration's draw record (ring slot (t-1) % draw_slots)
+  a.draws = c->buf.draws ? c->buf.draws + (size_t)((t >= 1 ? t - 1 : 0) % c->draw_slots) * c->buf.draw_slot_stride
+                         : nullptr;
+  a.draw_words = (int)c->draw_words;
+  a.planes = draw_planes(c->cfg.algorithm);
   a.eps = c->buf.eps;
   a.stats = c->buf.stats;
   a.stop_iter = c->buf.stop_iter;
@@ -2026,18 +2135,70 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   }
 }
 
-void launch_draw(const spgg_ctx* c, int t, hipStream_t s) {
-  hipLaunchKernelGGL(spgg_mt_draw_kernel, dim3(c->cfg.n_rep), dim3(kMtThreads), 0, s,
-                     c->buf.mt_state, c->buf.draws, (size_t)c->buf.draw_plane_stride, c->buf.eps,
-                     c->buf.stats, c->buf.stop_iter, c->n, c->cfg.iterations + 2, t, c->cfg.algorithm,
-                     c->stripes);
+GenArgs gen_args(const spgg_ctx* c) {
+  GenArgs g{};
+  g.mt_state = c->buf.mt_state;
+  g.snap = c->buf.mt_snap;
+  g.snap_stride = c->buf.mt_snap_stride;
+  g.snap_slots = c->snap_slots;
+  g.draws = c->buf.draws;
+  g.draw_stride = c->buf.draw_slot_stride;
+  g.draw_slots = c->draw_slots;
+  g.draw_words = (int)c->draw_words;
+  g.eps = c->buf.eps;
+  g.eps_slots = c->cfg.iterations + 2;
+  g.stop_iter = c->buf.stop_iter;
+  g.n = c->n;
+  g.alg = c->cfg.algorithm;
+  return g;
+}
+
+void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t s) {
+  hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep), dim3(kGenThreads), 0, s, gen_args(c), t0, t1,
+                     skip_stopped);
+}
+
+// MT19937 pipeline: generation of chunk q (iterations q*K+1 .. (q+1)*K) waits for the steps
+// of chunk q-2 (whose ring slots it reuses) and is enqueued when chunk q-1 starts, so it
+// overlaps the steps of chunk q-1; the steps of chunk q wait for it.
+int mt_lazy_init(spgg_ctx* c) {
+  if (c->gen_done[0]) return SPGG_OK;
+  int rc = SPGG_OK;
+  if (!c->gen_stream) {
+    rc = hip_check(c, hipStreamCreateWithFlags(&c->gen_stream, hipStreamNonBlocking), "hipStreamCreate(gen)");
+    if (rc) return rc;
+    c->own_gen_stream = true;
+  }
+  for (int i = 0; i < 2 && !rc; ++i) {
+    rc = hip_check(c, hipEventCreateWithFlags(&c->gen_done[i], hipEventDisableTiming), "hipEventCreate");
+    if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->step_done[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->gen_idle, hipEventDisableTiming), "hipEventCreate");
+  return rc;
+}
+
+void enqueue_gen_chunk(spgg_ctx* c, int q) {
+  const int K = c->gen_chunk;
+  const int t0 = q * K + 1, t1 = std::min((q + 1) * K, c->cfg.iterations);
+  if (q >= 2) (void)hipStreamWaitEvent(c->gen_stream, c->step_done[q & 1], 0);
+  launch_gen(c, t0, t1, 1, c->gen_stream);
+  (void)hipEventRecord(c->gen_done[q & 1], c->gen_stream);
+  c->gen_upto = t1;
 }
 
 }  // namespace
 
+#ifndef SPGG_BUILD_ID
+#define SPGG_BUILD_ID "unversioned"
+#endif
+
 extern "C" {
 
 int spgg_abi_version(void) { return SPGG_ABI_VERSION; }
+
+// "spgg-build:<id>" also lets build.py read the id from the file without loading it
+static const char kBuildTag[] = "spgg-build:" SPGG_BUILD_ID;
+const char* spgg_build_id(void) { return kBuildTag + 11; }
 
 int spgg_draw_planes(int32_t algorithm) {
   if (algorithm < SPGG_ALG_QLEARNING || algorithm > SPGG_ALG_DOUBLE_Q) return SPGG_E_ARG;
@@ -2094,6 +2255,15 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->cfg = *cfg;
   c->n = cfg->L * cfg->L;
   c->apt = apt;
+  // MT19937 pipeline depth (iterations per generator launch): SPGG_MT_CHUNK, default 8
+  if (const char* e = getenv("SPGG_MT_CHUNK")) c->gen_chunk = std::max(1, std::min(256, atoi(e)));
+  {  // a generator launch indexes its words in 32 bits (below 2^31)
+    const long long per_iter = draw_mt_words(c->n, draw_planes(cfg->algorithm));
+    c->gen_chunk = (int)std::max(1LL, std::min((long long)c->gen_chunk, ((1LL << 31) - (1LL << 16)) / per_iter));
+  }
+  c->draw_slots = 2 * c->gen_chunk;
+  c->snap_slots = 3 * c->gen_chunk + 1;
+  c->draw_words = draw_words_of(c->n, cfg->algorithm);
   choose_tile(cfg->L, kBlock * c->apt, &c->TW, &c->TH);
   if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;
@@ -2162,10 +2332,12 @@ int spgg_bind(spgg_ctx* c, const spgg_buffers* b) {
   if (!b->Q || !b->md || !b->atd || !b->eps || !b->stats || !b->stop_iter)
     return fail(c, SPGG_E_ARG, "spgg_bind: a required buffer is null");
   if (c->cfg.rng_mode != SPGG_RNG_PHILOX &&
-      (!b->draws || b->draw_plane_stride < (int64_t)c->cfg.n_rep * c->n))
-    return fail(c, SPGG_E_ARG, "spgg_bind: draw planes (stride >= n_rep*n) required for INJECT/MT19937");
-  if (c->cfg.rng_mode == SPGG_RNG_MT19937 && !b->mt_state)
-    return fail(c, SPGG_E_ARG, "spgg_bind: mt_state required for MT19937");
+      (!b->draws || b->draw_slot_stride < (int64_t)c->cfg.n_rep * c->draw_words))
+    return fail(c, SPGG_E_ARG, "spgg_bind: draw records (spgg_draw_layout slots, stride >= n_rep*words) required "
+                               "for INJECT/MT19937");
+  if (c->cfg.rng_mode == SPGG_RNG_MT19937 &&
+      (!b->mt_state || !b->mt_snap || b->mt_snap_stride < (int64_t)c->cfg.n_rep * 625))
+    return fail(c, SPGG_E_ARG, "spgg_bind: mt_state and mt_snap (stride >= n_rep*625) required for MT19937");
   if ((reinterpret_cast<uintptr_t>(b->Q) & 15) != 0)
     return fail(c, SPGG_E_ARG, "spgg_bind: the Q buffer must be 16-byte aligned");
   c->buf = *b;
@@ -2184,10 +2356,23 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
   else if (c->kappa_woke)
     return fail(c, SPGG_E_STATE, "spgg_step: a replica's kappa changed from 0 to nonzero mid-run");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
+  if (mt) {
+    int rc = mt_lazy_init(c);
+    if (rc) return rc;
+    if (t0 == 1) c->gen_upto = 0;  // a new run: generation restarts from mt_state
+  }
   if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
+  const int K = c->gen_chunk, T = c->cfg.iterations;
   for (int t = t0; t < t0 + n_steps; ++t) {
-    if (c->cfg.rng_mode == SPGG_RNG_MT19937) launch_draw(c, t, s);
+    if (mt) {
+      const int q = (t - 1) / K;
+      // this chunk and the next one enqueued (the next overlaps this chunk's steps)
+      while (c->gen_upto < std::min(T, (q + 2) * K)) enqueue_gen_chunk(c, c->gen_upto / K);
+      if (t == q * K + 1 || t == t0) (void)hipStreamWaitEvent(s, c->gen_done[q & 1], 0);
+    }
     launch_step(c, t, 0, s);
+    if (mt && (t % K == 0 || t == T)) (void)hipEventRecord(c->step_done[((t - 1) / K) & 1], s);
   }
   return hip_check(c, hipGetLastError(), "spgg_step launch");
 }
@@ -2198,7 +2383,16 @@ int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {
   if (t_last < 1 || t_last > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_flush: bad t_last");
   if (c->kappa_woke)  // the NI term would read a pending record that was never written
     return fail(c, SPGG_E_STATE, "spgg_flush: a replica's kappa changed from 0 to nonzero mid-run");
-  launch_step(c, t_last + 1, 1, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (c->cfg.rng_mode == SPGG_RNG_MT19937 && c->gen_done[0]) {
+    // the generator ran ahead: wait for it, then restore each replica's key to the one the
+    // reference holds (after its last executed iteration) from the snapshot ring
+    (void)hipEventRecord(c->gen_idle, c->gen_stream);
+    (void)hipStreamWaitEvent(s, c->gen_idle, 0);
+    hipLaunchKernelGGL(spgg_mt_final_kernel, dim3(c->cfg.n_rep), dim3(256), 0, s, gen_args(c), t_last);
+    c->gen_upto = 0;
+  }
+  launch_step(c, t_last + 1, 1, s);
   return hip_check(c, hipGetLastError(), "spgg_flush launch");
 }
 
@@ -2218,7 +2412,7 @@ int spgg_draw(spgg_ctx* c, int32_t t, void* stream) {
   if (!c->bound || c->cfg.rng_mode != SPGG_RNG_MT19937)
     return fail(c, SPGG_E_STATE, "spgg_draw needs a bound MT19937 context");
   if (t < 1 || t > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_draw: bad t");
-  launch_draw(c, t, reinterpret_cast<hipStream_t>(stream));
+  launch_gen(c, t, t, 0, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_draw launch");
 }
 
@@ -2251,12 +2445,36 @@ int spgg_tile_shape(const spgg_ctx* c, int32_t* tw, int32_t* th) {
   return SPGG_OK;
 }
 
+int spgg_draw_layout(const spgg_ctx* c, int32_t* slots, int64_t* words_per_rep, int32_t* snap_slots) {
+  if (!c || !slots || !words_per_rep || !snap_slots) return SPGG_E_ARG;
+  *slots = c->draw_slots;
+  *words_per_rep = c->draw_words;
+  *snap_slots = c->snap_slots;
+  return SPGG_OK;
+}
+
+int spgg_set_draw_stream(spgg_ctx* c, void* stream) {
+  if (!c) return SPGG_E_ARG;
+  if (c->cfg.rng_mode != SPGG_RNG_MT19937) return fail(c, SPGG_E_STATE, "spgg_set_draw_stream: MT19937 only");
+  if (c->gen_done[0] || c->gen_stream) return fail(c, SPGG_E_STATE, "spgg_set_draw_stream: set it before spgg_step");
+  c->gen_stream = reinterpret_cast<hipStream_t>(stream);
+  c->own_gen_stream = false;
+  return SPGG_OK;
+}
+
 int spgg_destroy(spgg_ctx* c) {
   if (!c) return SPGG_OK;
-  if (c->d_params || c->d_ring) {
+  if (c->d_params || c->d_ring || c->gen_stream || c->gen_done[0]) {
     (void)hipSetDevice(c->cfg.device);
+    if (c->gen_stream) (void)hipStreamSynchronize(c->gen_stream);  // no generator writes after return
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_ring) (void)hipFree(c->d_ring);
+    for (int i = 0; i < 2; ++i) {
+      if (c->gen_done[i]) (void)hipEventDestroy(c->gen_done[i]);
+      if (c->step_done[i]) (void)hipEventDestroy(c->step_done[i]);
+    }
+    if (c->gen_idle) (void)hipEventDestroy(c->gen_idle);
+    if (c->own_gen_stream) (void)hipStreamDestroy(c->gen_stream);
   }
   delete c;
   return SPGG_OK;

@@ -278,10 +278,9 @@ class BatchEngine:
         # pending NI record, in place: max(0, max_diff) and |alpha*td'| (diagnostic)
         self.md = torch.zeros((R, n), dtype=f64, device=d)
         self.atd = torch.zeros((R, n), dtype=torch.float32, device=d)
-        # draw planes of one iteration (device MT19937 / inject), spgg_abi.h
+        # draw records (device MT19937 / inject): a ring of bit planes, allocated in _create
+        # from the library's layout (spgg_draw_layout)
         self.n_planes = C.DRAW_PLANES[self.alg]
-        shape = (self.n_planes, R, n) if self.rng != "philox" else (1, 1, 1)
-        self.draws = torch.zeros(shape, dtype=u8, device=d)
         mt = np.zeros((R, 625), dtype=np.uint32)
         if self.rng == "mt19937":
             for k, s in enumerate(self.init):
@@ -336,6 +335,13 @@ class BatchEngine:
                 self.stats = torch.zeros((self.R, self.stripes, self.T + 2, C.NSTAT), dtype=torch.float64,
                                          device=self.dev)
                 self.stats[:, 0, 1, C.ST_NCOOP] = torch.from_numpy(self._ncoop0).to(self.dev)
+                slots, words, snaps = self._draw_layout(ctx)
+                self.draw_slots, self.draw_words = slots, words
+                rngd = self.rng != "philox"
+                self.draws = torch.zeros((slots, self.R, words) if rngd else (1, 1, 1), dtype=torch.int32,
+                                         device=self.dev)
+                self.mt_snap = torch.zeros((snaps, self.R, 625) if self.rng == "mt19937" else (1, 1, 1),
+                                           dtype=torch.int32, device=self.dev)
             elif layout != self.layout:
                 raise C.SpggError(f"replica group {g} got tiling {layout} != group 0's {self.layout} "
                                   "(tile, border-record doubles, stripes): shared buffer strides would disagree")
@@ -345,8 +351,10 @@ class BatchEngine:
                 b.pub[i] = self.pub[i][r0].data_ptr()
             b.Q, b.md, b.atd = self.Qb[r0].data_ptr(), self.md[r0].data_ptr(), self.atd[r0].data_ptr()
             b.draws = self.draws[0, min(r0, self.draws.shape[1] - 1)].data_ptr()
-            b.draw_plane_stride = self.draws.shape[1] * self.draws.shape[2]
+            b.draw_slot_stride = self.draws.shape[1] * self.draws.shape[2]
             b.mt_state = self.mt_state[r0].data_ptr()
+            b.mt_snap = self.mt_snap[0, min(r0, self.mt_snap.shape[1] - 1)].data_ptr()
+            b.mt_snap_stride = self.mt_snap.shape[1] * self.mt_snap.shape[2]
             b.eps, b.stats = self.eps[r0].data_ptr(), self.stats[r0].data_ptr()
             b.stop_iter = self.stop_iter[r0].data_ptr()
             C.check(self.lib.spgg_bind(ctx, b), ctx, "spgg_bind")
@@ -354,6 +362,20 @@ class BatchEngine:
         self.streams = streams
         self.ctx = self.groups[0]["ctx"]
         self.tile = self.layout[0]
+
+    def _draw_layout(self, ctx):
+        """(ring slots, u32 words per replica and slot, key-snapshot slots) of the draw records."""
+        slots, snaps, words = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        C.check(self.lib.spgg_draw_layout(ctx, ctypes.byref(slots), ctypes.byref(words), ctypes.byref(snaps)),
+                ctx, "spgg_draw_layout")
+        return int(slots.value), int(words.value), int(snaps.value)
+
+    def draw_record(self, t):
+        """(planes, R, n) uint8 0/1 view of iteration t's draw record (unpacked on the host)."""
+        x = self.draws[(t - 1) % self.draw_slots].cpu().numpy().view(np.uint32)
+        x = x.reshape(self.R, -1, self.n_planes).transpose(0, 2, 1)          # [R][planes][words]
+        bits = np.unpackbits(np.ascontiguousarray(x).view(np.uint8), axis=-1, bitorder="little")
+        return np.ascontiguousarray(bits[..., :self.n].transpose(1, 0, 2))
 
     def _layout(self, ctx):
         """(tile shape, border-record doubles per replica, history stripes) of a context."""
@@ -421,7 +443,13 @@ class BatchEngine:
                 planes[2 * j + 1, k] = s.rs.randint(0, 2, size=(L, L)).reshape(-1)
             if self.double_q:
                 planes[2, k] = s.rs.rand(L, L).reshape(-1) < 0.5
-        self.draws.copy_(torch.from_numpy(planes))
+        # bits, 32 agents per word, the planes of a word interleaved (spgg_abi.h draws)
+        nwords = self.draw_words // self.n_planes
+        pad = np.zeros((self.n_planes, self.R, nwords * 32), dtype=np.uint8)
+        pad[:, :, :self.n] = planes
+        words = np.packbits(pad, axis=-1, bitorder="little").view(np.uint32)    # [planes][R][words]
+        rec = np.ascontiguousarray(words.transpose(1, 2, 0)).reshape(self.R, -1)
+        self.draws[(t - 1) % self.draw_slots].copy_(torch.from_numpy(rec.view(np.int32)))
 
     def step(self, n_steps: int):
         """Enqueue the next n_steps iterations (no host sync except in inject mode)."""

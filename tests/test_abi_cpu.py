@@ -76,3 +76,22 @@ def test_create_failures_report_a_reason(monkeypatch):
     assert rc == _lib.E_ARG and "4 agents per thread" in msg
     with pytest.raises(_lib.SpggError, match="SPGG_APT=2"):
         _lib.check(rc, None, "spgg_create")
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_library_build_id_matches_sources(tmp_path):
+    """Freshness by content: the in-tree library carries the hash of the sources, flags and
+    defines it was built from (spgg_build_id), and the package refuses a library whose id
+    differs from the sources (build.py), whatever the file times say."""
+    import shutil
+    from spgg_amd import build as B
+    lib = _lib.load()
+    assert lib.spgg_build_id().decode() == B.build_id() == B.library_build_id(_lib.LIB_PATH)
+    assert not B.needs_build()
+    assert B.build_id(("SPGG_GEN_OUT=3",)) != B.build_id()     # defines are part of the id
+    stale = tmp_path / "lib.so"
+    data = open(_lib.LIB_PATH, "rb").read().replace(b"spgg-build:" + B.build_id().encode(),
+                                                   b"spgg-build:0000000000000000")
+    stale.write_bytes(data)
+    assert B.needs_build(str(stale))
+    assert B.library_build_id(str(stale)) == "0" * 16

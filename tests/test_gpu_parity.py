@@ -197,9 +197,10 @@ def test_device_mt_stream_matches_numpy(alg):
             want += [d["u2"] < e, d["b2"], d["u3"] < e, d["b3"]]
         if alg == "double_qlearning":
             want += [d["u_upd"] < 0.5]
-        assert eng.draws.shape[0] == len(want)
+        got = eng.draw_record(t)   # the ring slot's bit planes, unpacked
+        assert got.shape[0] == len(want)
         for p_, w in enumerate(want):
-            assert np.array_equal(eng.draws[p_, 0].cpu().numpy(), w.reshape(-1).astype(np.uint8)), (t, p_)
+            assert np.array_equal(got[p_, 0], w.reshape(-1).astype(np.uint8)), (t, p_)
     eng.close()
 
 

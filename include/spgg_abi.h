@@ -260,6 +260,9 @@ int spgg_history_finalize(spgg_ctx* ctx, int32_t t_last, void* hip_stream);
 /* Generate the draw record of iteration t only, from mt_state (advancing it), into its
  * ring slot (MT19937 mode; for tests -- spgg_step runs the pipelined generator itself). */
 int spgg_draw(spgg_ctx* ctx, int32_t t, void* hip_stream);
+/* The same for iterations t0..t1 in ONE generator launch (t1 - t0 < the generator's chunk,
+ * spgg_draw_layout slots / 2), as spgg_step's pipeline launches it (for tests). */
+int spgg_draw_range(spgg_ctx* ctx, int32_t t0, int32_t t1, void* hip_stream);
 
 /* Draw-record ring of INJECT / MT19937 contexts: ring slots (iterations), u32 words per
  * replica and slot, and key-snapshot slots (MT19937).  Replaces: the reference's per-step

@@ -34,7 +34,7 @@ NSTAT = 34
 EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create", "spgg_set_params",
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
-            "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream")
+            "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range")
 
 
 class Config(ctypes.Structure):
@@ -104,6 +104,8 @@ def load(path: str | None = None):
         lib.spgg_history_finalize.argtypes = [vp, i32, vp]
         lib.spgg_draw.restype = ctypes.c_int
         lib.spgg_draw.argtypes = [vp, i32, vp]
+        lib.spgg_draw_range.restype = ctypes.c_int
+        lib.spgg_draw_range.argtypes = [vp, i32, i32, vp]
         lib.spgg_payoff.restype = ctypes.c_int
         lib.spgg_payoff.argtypes = [vp, i32, vp, vp]
         lib.spgg_tile_shape.restype = ctypes.c_int

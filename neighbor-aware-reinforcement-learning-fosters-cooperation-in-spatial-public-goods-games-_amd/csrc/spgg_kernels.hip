@@ -1591,12 +1591,20 @@ __host__ __device__ inline int64_t draw_words_of(int n, int alg) {
 #define SPGG_GEN_ABLATE 0
 #endif
 #ifndef SPGG_GEN_NR
-#define SPGG_GEN_NR 2
+#define SPGG_GEN_NR 1
+#endif
+// Blocks between two progress publications of a lone recurrence wave (each publication waits
+// for the wave's LDS writes: one exposed LDS round trip per period); two recurrence waves
+// depend on each other's previous block and publish every block.
+#ifndef SPGG_GEN_PUB
+#define SPGG_GEN_PUB 4
 #endif
 constexpr int kGenOut = SPGG_GEN_OUT;            // output waves
 constexpr int kGenNR = SPGG_GEN_NR;              // recurrence waves (1 or 2)
 static_assert(kGenNR == 1 || kGenNR == 2, "recurrence waves: 1 or 2");
 constexpr int kGenSPW = 4 / kGenNR;              // slots per recurrence wave
+constexpr int kGenPub = kGenNR > 1 ? 1 : SPGG_GEN_PUB;
+static_assert(16 % kGenPub == 0, "publication period divides the unrolled block loop");
 constexpr int kGenThreads = 64 * (kGenNR + kGenOut);
 constexpr int kMtBlock = 227;                    // 624 - 397: words one dependency step produces
 constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
@@ -1614,7 +1622,7 @@ constexpr uint32_t kGenSpinMax = 1u << 23;
 // padding positions 227-255, so every LDS write is unconditional.
 __host__ __device__ constexpr int gen_slot_base(int s) { return s == 0 ? 0 : s == 1 ? 169 : s == 2 ? 58 : 122; }
 __host__ __device__ constexpr int gen_slot_len(int s) { return s == 0 ? 58 : s == 1 ? 58 : s == 2 ? 64 : 47; }
-__host__ __device__ constexpr int gen_slot_pad(int s) { return s == 0 ? 227 : s == 1 ? 233 : s == 2 ? 239 : 239 - 47; }
+__host__ __device__ constexpr int gen_slot_pad(int s) { return s == 0 ? 227 : s == 1 ? 233 : 239; }
 __device__ __forceinline__ int gen_position(int s, int lane) {
   return lane < gen_slot_len(s) ? gen_slot_base(s) + lane : gen_slot_pad(s) + lane - gen_slot_len(s);
 }
@@ -1640,13 +1648,17 @@ struct GenArgs {
 // Flags shared through LDS between the generator's waves: relaxed workgroup-scope atomics
 // on the __shared__ array itself (plain ds_read / ds_write; through a generic pointer they
 // become flat accesses with system-scope waits).  Every lane of a wave writes its own copy
-// (no branch around the store, so the wait counters stay exact); readers read lane 0's.  A
-// store is placed after every earlier LDS write of the wave (compiler barrier); one wave's
-// LDS operations complete in issue order, so a wave that reads the flag sees those writes.
+// (no branch around the store); readers read lane 0's.  A flag store is a release: it waits
+// until every earlier LDS access of the wave has completed (lgkmcnt(0); issue order alone
+// does not order another wave's view of two writes), and the compiler may not move an
+// access across it; a reader only touches the ring after its flag read returned.
 #define LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+// after a wait on a flag: no memory access of the wave may be moved above the wait by the
+// compiler (relaxed atomics do not order the plain ring accesses; the hardware does)
+#define GEN_FENCE() asm volatile("" ::: "memory")
 #define LDS_ST(x, v)                                                          \
   do {                                                                        \
-    asm volatile("" ::: "memory");                                            \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                        \
     __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
   } while (0)
 
@@ -1741,6 +1753,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       mind = poll_done();                                                                                 \
       if (mind + 1 < b) __builtin_amdgcn_s_sleep(1);                                                      \
     }                                                                                                     \
+    GEN_FENCE();                                                                                          \
     if (r == 0)                                                                                           \
       while (t <= t1 && 624u + kMtBlock * mind >= target) retire();                                       \
     const uint32_t F = 624u + kMtBlock * b;                                                               \
@@ -1753,6 +1766,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       lim = m > 0xffffffffu - (kGenNB - 1) * kMtBlock ? 0xffffffffu : m + (kGenNB - 1) * kMtBlock;        \
       if (F > lim) __builtin_amdgcn_s_sleep(2);                                                           \
     }                                                                                                     \
+    GEN_FENCE();                                                                                          \
     uint32_t na[kGenSPW], nb[kGenSPW];                                                                    \
     _Pragma("unroll") for (int i = 0; i < kGenSPW; ++i) {                                                 \
       constexpr int rb = ((U + 1 + kGenNB - 3) % kGenNB) * kGenPitch;                                     \
@@ -1768,9 +1782,13 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       cb[i] = nb[i];                                                                                      \
     }                                                                                                     \
     ++b;                                                                                                  \
-    LDS_ST(gen_done[r][lane], b);                                                                         \
-    if constexpr (kGenNR > 1) mind = poll_done(); /* used by the next block */                            \
-    else mind = b;                                                                                        \
+    if constexpr (kGenNR > 1) {                                                                           \
+      LDS_ST(gen_done[r][lane], b);                                                                       \
+      mind = poll_done(); /* used by the next block */                                                    \
+    } else {                                                                                              \
+      if ((U + 1) % kGenPub == 0) LDS_ST(gen_done[r][lane], b);                                           \
+      mind = b;                                                                                           \
+    }                                                                                                     \
   }
     static_assert(kGenNB == 16, "the block loop below is unrolled kGenNB times");
     for (;;) {
@@ -1781,11 +1799,13 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     }
 #undef SPGG_GEN_BLOCK
   rec_done:
+    LDS_ST(gen_done[r][lane], b);  // (a lone wave publishes every kGenPub blocks: the rest)
     if (r != 0) return;
     for (uint32_t spin = 0; mind < nblk && spin < kGenSpinMax; ++spin) {  // every wave's last block
       mind = poll_done();
       if (mind < nblk) __builtin_amdgcn_s_sleep(1);
     }
+    GEN_FENCE();
     while (t <= t1) retire();  // (the frontier covers every remaining target)
     for (int i = lane; i < 624; i += 64) key[i] = ring[gen_word_pos(key_mb + i)];
     if (lane == 0) key[624] = key_pos;
@@ -1815,6 +1835,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
         seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(m);
         if (seen <= last) __builtin_amdgcn_s_sleep(1);
       }
+      GEN_FENCE();
       if (!(SPGG_GEN_ABLATE & 1)) {
         // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
         const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
@@ -2407,12 +2428,15 @@ int spgg_history_finalize(spgg_ctx* c, int32_t t_last, void* stream) {
   return hip_check(c, hipGetLastError(), "spgg_history_finalize launch");
 }
 
-int spgg_draw(spgg_ctx* c, int32_t t, void* stream) {
+int spgg_draw(spgg_ctx* c, int32_t t, void* stream) { return spgg_draw_range(c, t, t, stream); }
+
+int spgg_draw_range(spgg_ctx* c, int32_t t0, int32_t t1, void* stream) {
   if (!c) return SPGG_E_ARG;
   if (!c->bound || c->cfg.rng_mode != SPGG_RNG_MT19937)
     return fail(c, SPGG_E_STATE, "spgg_draw needs a bound MT19937 context");
-  if (t < 1 || t > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_draw: bad t");
-  launch_gen(c, t, t, 0, reinterpret_cast<hipStream_t>(stream));
+  if (t0 < 1 || t1 < t0 || t1 > c->cfg.iterations || t1 - t0 + 1 > c->gen_chunk)
+    return fail(c, SPGG_E_ARG, "spgg_draw_range: 1 <= t0 <= t1 <= iterations, t1 - t0 < gen chunk");
+  launch_gen(c, t0, t1, 0, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_draw launch");
 }
 

@@ -204,6 +204,39 @@ def test_device_mt_stream_matches_numpy(alg):
     eng.close()
 
 
+@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("L", [24, 37, 200])
+def test_device_mt_multi_iteration_launch(alg, L):
+    """spgg_draw_range: one generator launch producing several iterations (as spgg_step's
+    pipeline runs it: the LDS ring wraps many times, key blocks roll over between iterations)
+    reproduces every RandomState draw of every iteration, and leaves the key RandomState holds."""
+    from spgg_amd import _lib as C
+    T = 8
+    eng = BatchEngine(L, T, [_runner_params(seed=3, epsilon=0.7, epsilon_decay=0.9)], use_second_order=False,
+                      rng="mt19937", algorithm=alg)
+    try:
+        rs = np.random.RandomState(3)
+        reference_init(L, rs, algorithm=alg)
+        t0, t1 = 1, min(T, eng.draw_slots // 2)
+        C.check(eng.lib.spgg_draw_range(eng.ctx, t0, t1, eng.stream), eng.ctx, "spgg_draw_range")
+        for t in range(t0, t1 + 1):
+            d = O.draw_step(rs, L, alg)
+            e = eng.eps_host[0, t]
+            want = [d["u"] < e, d["b"]]
+            if alg == "sarsa":
+                want += [d["u2"] < e, d["b2"], d["u3"] < e, d["b3"]]
+            if alg == "double_qlearning":
+                want += [d["u_upd"] < 0.5]
+            got = eng.draw_record(t)
+            for p_, w in enumerate(want):
+                assert np.array_equal(got[p_, 0], w.reshape(-1).astype(np.uint8)), (t, p_)
+        key, pos = eng.mt_state_host(0)
+        st = rs.get_state()
+        assert pos == st[2] and np.array_equal(key, st[1])
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("apt", ["1", "max"])
 @pytest.mark.parametrize("L,T,M2", [(200, 150, False), (200, 60, True), (1000, 3, False)])
 def test_full_size_bit_exact(L, T, M2, apt, monkeypatch):

@@ -1,0 +1,216 @@
+"""A model check of the MT19937 draw generator's wave protocol (csrc/spgg_kernels.hip,
+spgg_mt_gen_kernel) on the CPU: the recurrence and output waves are restated as coroutines
+that yield at every LDS access, run under random interleavings over a sequentially
+consistent LDS, and their outputs are compared with numpy's RandomState stream.
+
+What it checks is the kernel's index arithmetic (the 256-word ring blocks and their mirror,
+the slot/padding positions gen_slot_*, gen_word_pos, gen_spill, the key-block bookkeeping of
+multi-iteration launches) and its synchronisation (gen_done progress, gen_need flow control,
+the recurrence waves' block-of-slack rule), independent of timing.  The hardware ordering the
+kernel relies on beyond sequential consistency (a flag store waits for the wave's earlier LDS
+writes) is exercised by the -m gpu tests.  (A padding-position bug of the first version of
+this kernel -- slot 3's spare lanes overwriting slot 1's words -- is the kind of defect this
+finds: it failed every interleaving here and only some runs on the GPU.)"""
+import random
+
+import numpy as np
+import pytest
+
+NB, P, MB = 16, 256, 227        # kGenNB, kGenPitch, kMtBlock
+RING = P * (NB + 1)
+
+
+def spill(o):                    # gen_spill
+    return o + (P - MB if o >= MB else 0)
+
+
+def word_pos(k):                 # gen_word_pos
+    kk = k + 57
+    B = kk // MB
+    return P * ((B + NB - 3) % NB) + (kk - B * MB)
+
+
+SLOT_BASE, SLOT_LEN, SLOT_PAD = (0, 169, 58, 122), (58, 58, 64, 47), (227, 233, 239, 239)   # gen_slot_*
+
+
+def position(s, lane):           # gen_position
+    return SLOT_BASE[s] + lane if lane < SLOT_LEN[s] else SLOT_PAD[s] + lane - SLOT_LEN[s]
+
+
+def temper(y):
+    y ^= y >> 11
+    y ^= (y << 7) & 0x9D2C5680
+    y ^= (y << 15) & 0xEFC60000
+    y ^= y >> 18
+    return y & 0xFFFFFFFF
+
+
+def mt_next(far, a, b):
+    y = (a & 0x80000000) | (b & 0x7FFFFFFF)
+    return (far ^ (y >> 1) ^ (0x9908B0DF if b & 1 else 0)) & 0xFFFFFFFF
+
+
+def plane_word0(n, p):
+    return n * (p // 2 * 3 + (p & 1) * 2)
+
+
+def run_model(n, planes, t0, t1, key, pos0, seed, NR, NOUT=7, PUB=4):
+    rnd = random.Random(seed)
+    SPW = 4 // NR
+    ring = [0] * RING
+    for i in range(624):
+        ring[word_pos(i)] = key[i]
+    gen_done = [0] * NR
+    gen_need = [0] * NOUT
+    W = plane_word0(n, planes) if planes % 2 == 0 else n * (planes // 2 * 3 + 2)
+    E_last = pos0 + (t1 - t0 + 1) * W
+    target_last = ((E_last - 1) // 624) * 624 + 624
+    nblk = (target_last - 624 + MB - 1) // MB if target_last > 624 else 0
+    out, keys = {}, {}
+
+    def rec(r):
+        lanes = [(i, lane, position(r * SPW + i, lane)) for i in range(SPW) for lane in range(64)]
+        prev = {(i, l): ring[j + (NB - 1) * P] for i, l, j in lanes}
+        ca = {(i, l): ring[spill(j + 57) + (NB - 3) * P] for i, l, j in lanes}
+        cb = {(i, l): ring[spill(j + 58) + (NB - 3) * P] for i, l, j in lanes}
+        yield
+        E = pos0 + W
+        mb = ((E - 1) // 624) * 624
+        target = mb + 624
+        lim = mind = b = 0
+        t = t0
+        key_mb, key_pos = 0, pos0
+
+        def retire():
+            nonlocal t, E, mb, target, key_mb, key_pos
+            keys[t] = ([ring[word_pos(mb + i)] for i in range(624)], E - mb)
+            key_mb, key_pos = mb, E - mb
+            t += 1
+            E += W
+            mb = ((E - 1) // 624) * 624
+            target = mb + 624
+
+        while b != nblk:
+            while NR > 1 and mind + 1 < b:
+                mind = min(gen_done)
+                yield
+            if r == 0:
+                while t <= t1 and 624 + MB * mind >= target:
+                    retire()
+                    yield
+            F = 624 + MB * b
+            while F > lim:
+                m = min(gen_need)
+                lim = 0xFFFFFFFF if m > 0xFFFFFFFF - (NB - 1) * MB else m + (NB - 1) * MB
+                yield
+            U = b % NB
+            rb = ((U + 1 + NB - 3) % NB) * P
+            na = {(i, l): ring[spill(j + 57) + rb] for i, l, j in lanes}
+            nb_ = {(i, l): ring[spill(j + 58) + rb] for i, l, j in lanes}
+            yield
+            for i, l, j in lanes:
+                x = mt_next(prev[i, l], ca[i, l], cb[i, l])
+                prev[i, l] = x
+                ring[j + U * P] = x
+                if U == 0:
+                    ring[j + NB * P] = x
+                ca[i, l], cb[i, l] = na[i, l], nb_[i, l]
+            yield
+            b += 1
+            if NR > 1 or (U + 1) % PUB == 0:
+                gen_done[r] = b
+            yield
+            mind = min(gen_done) if NR > 1 else b
+        gen_done[r] = b
+        if r != 0:
+            return
+        while mind < nblk:
+            mind = min(gen_done)
+            yield
+        while t <= t1:
+            retire()
+
+    def outw(ow):
+        nchunk = (n + 63) // 64
+        kpos, seen = pos0, 624
+        for t in range(t0, t1 + 1):
+            p, c = 0, ow
+            while p < planes and c >= nchunk:
+                c -= nchunk
+                p += 1
+            while p < planes:
+                cnt, dbl = min(64, n - 64 * c), (p & 1) == 0
+                first = kpos + plane_word0(n, p) + (128 if dbl else 64) * c
+                last = first + (2 if dbl else 1) * cnt - 1
+                gen_need[ow] = first
+                yield
+                while seen <= last:
+                    seen = 624 + MB * min(gen_done)
+                    yield
+                kk = first + 57
+                B = kk // MB
+                o0, rbase = kk - B * MB, P * ((B + NB - 3) % NB)
+                if dbl:
+                    out[t, p, c] = [(temper(ring[rbase + spill(o0 + 2 * l)]), temper(ring[rbase + spill(o0 + 2 * l + 1)]))
+                                    for l in range(cnt)]
+                else:
+                    out[t, p, c] = [temper(ring[rbase + spill(o0 + l)]) for l in range(cnt)]
+                yield
+                c += NOUT
+                while p < planes and c >= nchunk:
+                    c -= nchunk
+                    p += 1
+            kpos += W
+        gen_need[ow] = 0xFFFFFFFF
+
+    waves = [rec(r) for r in range(NR)] + [outw(w) for w in range(NOUT)]
+    alive = list(range(len(waves)))
+    while alive:
+        i = rnd.choice(alive)
+        try:
+            next(waves[i])
+        except StopIteration:
+            alive.remove(i)
+    return out, keys
+
+
+@pytest.mark.parametrize("NR", [1, 2])
+@pytest.mark.parametrize("n,planes", [(100, 2), (576, 2), (300, 6), (250, 3)])
+def test_generator_protocol_model(NR, n, planes):
+    T = 4
+    for seed in range(2):
+        rs = np.random.RandomState(seed + 11)
+        rs.uniform(size=(seed * 37) % 500)          # start mid-block (pos != 624)
+        st = rs.get_state()
+        key, pos = [int(x) for x in st[1]], int(st[2])
+        out, keys = run_model(n, planes, 1, T, key, pos, seed, NR)
+        W = n * (planes // 2 * 3 + (planes & 1) * 2)
+        nchunk = (n + 63) // 64
+        for t in range(1, T + 1):
+            words = rs.randint(0, 2 ** 32, size=W, dtype=np.uint64)   # the raw 32-bit outputs
+            for p in range(planes):
+                base = plane_word0(n, p)
+                for c in range(nchunk):
+                    cnt = min(64, n - 64 * c)
+                    if p % 2 == 0:
+                        want = [(int(words[base + 128 * c + 2 * l]), int(words[base + 128 * c + 2 * l + 1]))
+                                for l in range(cnt)]
+                    else:
+                        want = [int(words[base + 64 * c + l]) for l in range(cnt)]
+                    assert out[t, p, c] == want, (seed, t, p, c)
+            k, ps = keys[t]
+            s = rs.get_state()
+            assert ps == int(s[2]) and k == [int(x) for x in s[1]], (seed, t)
+
+
+def test_slot_positions_partition_the_block():
+    """Every (slot, lane) owns its own position: the 227 real positions once each, the 29
+    spare lanes the padding 227-255 (a spare lane writing a real position races its owner)."""
+    pos = [position(s, lane) for s in range(4) for lane in range(64)]
+    assert sorted(pos) == list(range(256))
+    real = [position(s, lane) for s in range(4) for lane in range(SLOT_LEN[s])]
+    assert sorted(real) == list(range(MB))
+    # slots 0 and 1 (one wave) hold positions 0-57 and 169-226: the positions that need the
+    # block two back read only that wave's own words
+    assert {position(0, l) for l in range(58)} == set(range(58))
+    assert {position(1, l) for l in range(58)} == set(range(169, 227))

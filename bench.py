@@ -201,6 +201,12 @@ def main():
     eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng,
                       streams=args.streams, replica_offset=rank * len(reps))
     n_agents = len(reps) * L * L
+    mt_layout = None
+    if args.rng == "mt19937":  # the draw generator's chains (spgg_mt_chains)
+        import ctypes
+        ch, per = ctypes.c_int32(), ctypes.c_int32()
+        eng.lib.spgg_mt_chains(eng.ctx, ctypes.byref(ch), ctypes.byref(per))
+        mt_layout = {"chains_per_replica": ch.value, "iterations_per_chain": per.value}
 
     eng.step(W)
     torch.cuda.synchronize()
@@ -261,7 +267,7 @@ def main():
             "config": {"workload": desc, "L": L, "replicas_per_gpu": len(reps),
                        "agents_per_gpu": n_agents, "second_order": M2, "state": state,
                        "rng": args.rng, "streams_per_gpu": resident, "replica_groups": groups,
-                       "cache_waves": waves,
+                       "cache_waves": waves, "mt_chains": mt_layout,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -273,8 +279,9 @@ def main():
                          "kernel": (f"spgg_step_kernel, {resident} concurrent launches per iteration "
                                     f"(one per replica group/stream)" if args.rng == "philox" else
                                     f"spgg_step_kernel ({resident} concurrent launches per iteration) + "
-                                    f"spgg_mt_gen_kernel (one launch per 8 iterations per group, on its own "
-                                    f"stream)"),
+                                    f"spgg_mt_gen_kernel (one launch per chunk of {mt_layout['chains_per_replica']} "
+                                    f"chains x {mt_layout['iterations_per_chain']} iterations per group) + "
+                                    f"spgg_mt_jump_kernel, on their own stream"),
                          "device_ms_per_step": per_step_dev_s * 1e3},
         }
         T_full = FULL_RUN_ITERS.get(args.config, 0) if args.full_run < 0 else args.full_run

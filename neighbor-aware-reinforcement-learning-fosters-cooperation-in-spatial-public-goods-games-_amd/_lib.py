@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
@@ -34,7 +34,8 @@ NSTAT = 34
 EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create", "spgg_set_params",
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
-            "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range")
+            "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range",
+            "spgg_mt_chains", "spgg_mt_jump_poly")
 
 
 class Config(ctypes.Structure):
@@ -120,6 +121,10 @@ def load(path: str | None = None):
         lib.spgg_pub_doubles.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         lib.spgg_draw_layout.restype = ctypes.c_int
         lib.spgg_draw_layout.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32)]
+        lib.spgg_mt_chains.restype = ctypes.c_int
+        lib.spgg_mt_chains.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        lib.spgg_mt_jump_poly.restype = ctypes.c_int
+        lib.spgg_mt_jump_poly.argtypes = [ctypes.c_int64, vp]
         lib.spgg_set_draw_stream.restype = ctypes.c_int
         lib.spgg_set_draw_stream.argtypes = [vp, vp]
         lib.spgg_build_id.restype = ctypes.c_char_p

@@ -13,7 +13,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
-SRC = [os.path.join(PKG_DIR, "csrc", "spgg_kernels.hip")]
+SRC = [os.path.join(PKG_DIR, "csrc", "spgg_kernels.hip"),
+       os.path.join(PKG_DIR, "csrc", "spgg_mt.hip")]   # MT19937 jump-ahead (its own object)
 INC = os.path.join(ROOT, "include")
 OUT = os.path.join(PKG_DIR, "libspgg_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -28,7 +29,8 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-munsafe-fp-atomics"]
 
 
-DEPS = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h")]
+DEPS = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h"),
+              os.path.join(PKG_DIR, "csrc", "spgg_mt.h")]
 
 
 def build_id(defines=()):
@@ -63,9 +65,10 @@ def build(force=False, verbose=True, out=OUT, defines=()):
         return out
     extra = [f"-D{d}" for d in defines] + [f'-DSPGG_BUILD_ID="{build_id(defines)}"']
     with tempfile.TemporaryDirectory() as tmp:
-        objs = [os.path.join(tmp, f"tu{k}.o") for k in TUS]
+        objs = [os.path.join(tmp, f"tu{k}.o") for k in TUS] + [os.path.join(tmp, "mt.o")]
         cmds = [[HIPCC, *FLAGS, *extra, f"-DSPGG_TU={k}", f"-I{INC}", "-c", SRC[0], "-o", o]
                 for k, o in zip(TUS, objs)]
+        cmds.append([HIPCC, *FLAGS, *extra, f"-I{INC}", "-c", SRC[1], "-o", objs[-1]])
         if verbose:
             print(" ".join(cmds[0]).replace("-DSPGG_TU=0", "-DSPGG_TU={0,1,2,3,9}"), flush=True)
         jobs = max(1, min(len(cmds), os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "8"))))

@@ -40,6 +40,7 @@
 
 #include "spgg_abi.h"
 #include "spgg_device.h"
+#include "spgg_mt.h"
 
 using namespace spgg;
 
@@ -1559,11 +1560,7 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-// x[k+624] = x[k+397] ^ twist(x[k], x[k+1]): upper bit of x[k], lower 31 of x[k+1]
-__device__ __forceinline__ uint32_t mt_next(uint32_t far, uint32_t lo_k, uint32_t lo_k1) {
-  const uint32_t y = (lo_k & 0x80000000u) | (lo_k1 & 0x7fffffffu);
-  return far ^ (y >> 1) ^ ((lo_k1 & 1u) ? 0x9908b0dfu : 0u);
-}
+using spgg_mt::mt_next;
 
 // Draw program of one iteration, in the reference's order: plane i is rand(L,L)
 // compared with a threshold (2 words per value, i even) or randint(0,2,(L,L))
@@ -1631,7 +1628,11 @@ __device__ __forceinline__ int gen_position(int s, int lane) {
 __device__ __forceinline__ uint32_t gen_spill(uint32_t o) { return o + (o >= (uint32_t)kMtBlock ? kGenPitch - kMtBlock : 0u); }
 
 struct GenArgs {
-  uint32_t* mt_state;      // [rep][625] running key + pos
+  const uint32_t* key_in;  // [rep][625] chain 0's key + pos: mt_state, or the chunk's key buffer
+  uint32_t* key_out;       // [rep][625] the key after the launch's last iteration (its last chain)
+  const uint32_t* parts;   // chains >= 1: start windows, [rep][chain][kSplits][624] XOR parts
+  const uint32_t* run_pos0;  // [rep] first word of the run's iteration 1 in its key block
+  int chains, per_chain;   // chain c: iterations t0 + c*per_chain .. (+ per_chain - 1)
   uint32_t* snap;          // snapshot slot s of replica rep: snap + s*snap_stride + rep*625
   int64_t snap_stride;
   int snap_slots;
@@ -1669,35 +1670,64 @@ __device__ __forceinline__ uint32_t gen_word_pos(uint32_t k) {
   return (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB) + (kk - B * kMtBlock);
 }
 
-// Iterations t0..t1 of every replica (blockIdx.x), from the key in mt_state; writes the
-// draw records, the key snapshots (slot t % snap_slots = the key after iteration t;
-// t0 == 1 also slot 0 = the initial key) and the advanced key.  Word indices are
-// absolute within the launch (the host keeps a launch below 2^31 words: gen_chunk).
-// skip_stopped: replicas already absorbed are left alone (their draws are never read).
+// Iterations t0..t1 of every replica, from its key; writes the draw records, the key
+// snapshots (slot t % snap_slots = the key after iteration t; t0 == 1 also slot 0 = the
+// initial key) and the advanced key.  blockIdx.x = rep * chains + c: chain c runs
+// iterations t0 + c*per_chain .. (+ per_chain - 1) from its window -- chain 0 from key_in
+// (an aligned key block + pos), chain c >= 1 from the XOR of its parts: the window that
+// starts at its first draw word, whose offset within the reference's 624-word key blocks
+// is ph.  Word indices are relative to the chain's window (the host keeps a chain below
+// 2^31 words).  skip_stopped: replicas already absorbed are left alone (their draws are
+// never read).
 __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int t0, int t1, int skip_stopped) {
   __shared__ uint32_t ring[kGenRing];
   __shared__ uint32_t gen_done[kGenNR][64];   // blocks recurrence wave r has completed (per lane)
   __shared__ uint32_t gen_need[kGenOut][64];  // output wave w reads no word below this (per lane)
-  const int rep = blockIdx.x, tid = threadIdx.x;
-  if (skip_stopped && g.stop_iter[rep] != 0) return;
-  uint32_t* key = g.mt_state + (size_t)rep * 625;
-  for (int i = tid; i < 624; i += kGenThreads) ring[gen_word_pos(i)] = key[i];
-  if (tid < 64 * kGenNR) gen_done[tid >> 6][tid & 63] = 0;
-  if (tid < 64 * kGenOut) gen_need[tid >> 6][tid & 63] = 0;
-  if (t0 == 1) {
-    uint32_t* s0 = g.snap + (size_t)rep * 625;
-    for (int i = tid; i < 625; i += kGenThreads) s0[i] = key[i];
+  __shared__ uint32_t pos_sh;
+  const int rep = blockIdx.x / g.chains, ch = blockIdx.x - rep * g.chains, tid = threadIdx.x;
+  bool last_chain;  // the chain whose iterations end the launch: it writes key_out
+  {
+    const int ct0 = t0 + ch * g.per_chain;
+    if (ct0 > t1) return;
+    last_chain = ct0 + g.per_chain - 1 >= t1;
+    t1 = min(t1, ct0 + g.per_chain - 1);
+    t0 = ct0;
   }
-  const uint32_t pos0 = key[624];  // next word to consume (624: the block is exhausted)
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (skip_stopped && g.stop_iter[rep] != 0) return;
   const int planes = draw_planes(g.alg);
   const uint32_t W = (uint32_t)draw_mt_words(g.n, planes);
+  uint32_t ph = 0;  // offset of the window's first word within a key block
+  if (ch == 0) {
+    const uint32_t* key = g.key_in + (size_t)rep * 625;
+    for (int i = tid; i < 624; i += kGenThreads) ring[gen_word_pos(i)] = key[i];
+    if (tid == 0) pos_sh = key[624];  // next word to consume (624: the block is exhausted)
+    if (t0 == 1) {
+      uint32_t* s0 = g.snap + (size_t)rep * 625;
+      for (int i = tid; i < 625; i += kGenThreads) s0[i] = key[i];
+    }
+  } else {
+    const uint32_t* pp = g.parts + (size_t)(rep * g.chains + ch) * spgg_mt::kSplits * 624;
+    for (int i = tid; i < 624; i += kGenThreads) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int p = 0; p < spgg_mt::kSplits; ++p) v ^= pp[p * 624 + i];
+      ring[gen_word_pos(i)] = v;
+    }
+    if (tid == 0) pos_sh = 0;
+    ph = (uint32_t)(((uint64_t)g.run_pos0[rep] + (uint64_t)(t0 - 1) * W) % 624u);
+  }
+  if (tid < 64 * kGenNR) gen_done[tid >> 6][tid & 63] = 0;
+  if (tid < 64 * kGenOut) gen_need[tid >> 6][tid & 63] = 0;
+  __syncthreads();
+  const uint32_t pos0 = pos_sh;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  // first word of the key block holding word E - 1 (window-relative; >= 0: W >= 624 for chains)
+  auto key_block = [ph](uint32_t E) { return ((E - 1 + ph) / 624) * 624 - ph; };
   // blocks of 227 words this launch generates: through the key block of its last iteration
   uint32_t nblk;
   {
     const uint32_t E_last = pos0 + (uint32_t)(t1 - t0 + 1) * W;
-    const uint32_t target_last = ((E_last - 1) / 624) * 624 + 624;
+    const uint32_t target_last = key_block(E_last) + 624;
     nblk = target_last > 624 ? (target_last - 624 + kMtBlock - 1) / kMtBlock : 0;
   }
   if (wave < kGenNR) {
@@ -1717,7 +1747,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       cb[i] = pb[i][(kGenNB - 3) * kGenPitch];
     }
     uint32_t E = pos0 + W;
-    uint32_t mb = ((E - 1) / 624) * 624, target = mb + 624;
+    uint32_t mb = key_block(E), target = mb + 624;
     uint32_t lim = 0;   // largest F whose block may be written (output waves' reads)
     uint32_t mind = 0;  // blocks every recurrence wave has completed (as last read)
     int t = t0;
@@ -1736,7 +1766,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       key_pos = E - mb;
       ++t;
       E += W;
-      mb = ((E - 1) / 624) * 624;
+      mb = key_block(E);
       target = mb + 624;
     };
     auto poll_done = [&]() {  // min over the recurrence waves' completed blocks
@@ -1807,8 +1837,11 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     }
     GEN_FENCE();
     while (t <= t1) retire();  // (the frontier covers every remaining target)
-    for (int i = lane; i < 624; i += 64) key[i] = ring[gen_word_pos(key_mb + i)];
-    if (lane == 0) key[624] = key_pos;
+    if (last_chain) {
+      uint32_t* key = g.key_out + (size_t)rep * 625;
+      for (int i = lane; i < 624; i += 64) key[i] = ring[gen_word_pos(key_mb + i)];
+      if (lane == 0) key[624] = key_pos;
+    }
     return;
   }
   // ---- output waves: chunks ow, ow + kGenOut, ... of each iteration, plane-major --------
@@ -1867,7 +1900,7 @@ __global__ void spgg_mt_final_kernel(GenArgs g, int t_last) {
   const int st = g.stop_iter[rep];
   const int src = st ? st - 1 : t_last;
   const uint32_t* sn = g.snap + (size_t)(src % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
-  uint32_t* key = g.mt_state + (size_t)rep * 625;
+  uint32_t* key = g.key_out + (size_t)rep * 625;
   for (int i = threadIdx.x; i < 625; i += blockDim.x) key[i] = sn[i];
 }
 
@@ -1958,8 +1991,15 @@ struct spgg_ctx {
   bool params_set = false;
   // MT19937 draw pipeline: the generator runs gen_chunk iterations per launch on its own
   // stream, one chunk ahead of the steps; draw records in a ring of draw_slots = 2 chunks,
-  // key snapshots in a ring of snap_slots (spgg_draw_layout)
+  // key snapshots in a ring of snap_slots (spgg_draw_layout).  A chunk is chains x
+  // per_chain iterations: chain c of replica rep is workgroup rep*chains + c, started from
+  // the window its jump produced (spgg_mt.h)
   int gen_chunk = 8, draw_slots = 16, snap_slots = 25;
+  int chains = 1, per_chain = 8, jump_levels = 0;  // jump_levels = log2(chains)
+  uint32_t* d_parts[2] = {nullptr, nullptr};  // chain start windows of chunks q (q & 1)
+  uint32_t* d_keybuf[2] = {nullptr, nullptr}; // chain 0's key of chunk q ([q & 1]; chunk 0: mt_state)
+  uint32_t* d_run_pos0 = nullptr;
+  uint32_t* d_polys = nullptr;                // x^(2^j per_chain W - 1) mod phi, j = 0..jump_levels
   int64_t draw_words = 0;            // u32 words of one replica's draw record
   hipStream_t gen_stream = nullptr;  // the generator's stream (library-owned unless set)
   bool own_gen_stream = false;
@@ -2011,6 +2051,46 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
 // one agent per thread, 8 replicas (320 tiles, M=2) 16.2 -> 17.0, one L=1000
 // replica (1000 tiles) 28.1 -> 53.9.  SPGG_APT=1 / =<max> forces either.
 constexpr long long kSmallBatchTiles = 128;
+
+// MT19937 generator layout (spgg_mt_chains).  One chain generates a replica's draws at
+// ~200 ns per 227 words (measured: 119-215 ns with the steps running), i.e. ~W/227*0.2 us
+// per iteration of W words; the steps take ~15 ps per agent of the batch (cfg3: 62 us for
+// 4.2e6 agents), >= ~8 us.  Chains per replica: a power of two with twice the needed rate.
+// A chain covers >= ~1e6 words (a jump costs ~20 us on 8 workgroups), the draw ring
+// (2 chunks) stays <= 96 MB.  Lattices under 4096 words per iteration keep one chain.
+void choose_mt_chains(spgg_ctx* c) {
+  const spgg_config& cfg = c->cfg;
+  const long long W = draw_mt_words(c->n, draw_planes(cfg.algorithm));
+  int chains = 1, per = 8;
+  if (W >= 4096) {
+    const double gen_ns = W / 227.0 * 200.0;
+    const long long batch = cfg.batch_reps > 0 ? cfg.batch_reps : cfg.n_rep;
+    const double step_ns = std::max(8000.0, (double)batch * c->n * 0.015);
+    const double need = 2.0 * gen_ns / step_ns;
+    while (chains < 256 && chains < need) chains *= 2;
+    if (chains > 1) per = (int)std::max(1LL, (1000000 + W - 1) / W);
+    const double rec = draw_words_of(c->n, cfg.algorithm) * 4.0 * cfg.n_rep;  // bytes per iteration
+    while (chains > 1 && 2.0 * chains * per * rec > 96e6) {
+      if (per > 1) per = std::max(1, per / 2);
+      else chains /= 2;
+    }
+  }
+  if (const char* e = getenv("SPGG_MT_CHAINS")) {
+    int v = atoi(e), p2 = 1;
+    while (p2 < 256 && p2 < v) p2 *= 2;
+    chains = W >= 624 ? std::max(1, p2) : 1;  // (a chain's first key block must lie in its window)
+  }
+  if (const char* e = getenv("SPGG_MT_PER_CHAIN")) per = std::max(1, std::min(4096, atoi(e)));
+  if (chains == 1)
+    if (const char* e = getenv("SPGG_MT_CHUNK")) per = std::max(1, std::min(256, atoi(e)));
+  // a chain indexes its words in 32 bits (below 2^31)
+  per = (int)std::max(1LL, std::min((long long)per, ((1LL << 31) - (1LL << 16)) / W));
+  c->chains = chains;
+  c->per_chain = per;
+  c->gen_chunk = chains * per;
+  c->jump_levels = 0;
+  while ((1 << c->jump_levels) < chains) ++c->jump_levels;
+}
 
 // Workgroups per history-record stripe (spgg_stat_stripes).
 constexpr int kTilesPerStripe = 64;
@@ -2156,9 +2236,15 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   }
 }
 
-GenArgs gen_args(const spgg_ctx* c) {
+// q: the chunk a pipelined launch generates (-1: a single-chain launch in place on mt_state)
+GenArgs gen_args(const spgg_ctx* c, int q = -1) {
   GenArgs g{};
-  g.mt_state = c->buf.mt_state;
+  g.key_in = q <= 0 ? c->buf.mt_state : c->d_keybuf[q & 1];
+  g.key_out = q < 0 ? c->buf.mt_state : c->d_keybuf[(q + 1) & 1];
+  g.parts = q < 0 ? nullptr : c->d_parts[q & 1];
+  g.run_pos0 = c->d_run_pos0;
+  g.chains = q < 0 ? 1 : c->chains;
+  g.per_chain = q < 0 ? c->gen_chunk : c->per_chain;
   g.snap = c->buf.mt_snap;
   g.snap_stride = c->buf.mt_snap_stride;
   g.snap_slots = c->snap_slots;
@@ -2174,8 +2260,9 @@ GenArgs gen_args(const spgg_ctx* c) {
   return g;
 }
 
-void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t s) {
-  hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep), dim3(kGenThreads), 0, s, gen_args(c), t0, t1,
+void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t s, int q = -1) {
+  const GenArgs g = gen_args(c, q);
+  hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep * g.chains), dim3(kGenThreads), 0, s, g, t0, t1,
                      skip_stopped);
 }
 
@@ -2195,15 +2282,48 @@ int mt_lazy_init(spgg_ctx* c) {
     if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->step_done[i], hipEventDisableTiming), "hipEventCreate");
   }
   if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->gen_idle, hipEventDisableTiming), "hipEventCreate");
-  return rc;
+  if (rc || c->chains == 1) return rc;
+  // chained generator: start windows, chunk keys, and the jump polynomials
+  const size_t R = c->cfg.n_rep, win = R * c->chains * spgg_mt::kSplits * 624;
+  for (int i = 0; i < 2 && !rc; ++i) {
+    rc = hip_check(c, hipMalloc(&c->d_parts[i], win * 4), "hipMalloc(mt parts)");
+    if (!rc) rc = hip_check(c, hipMalloc(&c->d_keybuf[i], R * 625 * 4), "hipMalloc(mt keys)");
+  }
+  if (!rc) rc = hip_check(c, hipMalloc(&c->d_run_pos0, R * 4), "hipMalloc(mt pos)");
+  if (!rc) rc = hip_check(c, hipMalloc(&c->d_polys, (size_t)(c->jump_levels + 1) * 624 * 4), "hipMalloc(mt polys)");
+  if (rc) return rc;
+  const uint64_t W = (uint64_t)draw_mt_words(c->n, draw_planes(c->cfg.algorithm));
+  std::vector<uint32_t> polys((size_t)(c->jump_levels + 1) * 624);
+  for (int j = 0; j <= c->jump_levels; ++j) {
+    spgg_mt::jump_poly(((uint64_t)c->per_chain * W << j) - 1, polys.data() + (size_t)j * 624);
+    bool nz = false;
+    for (int i = 0; i < 624; ++i) nz |= polys[(size_t)j * 624 + i] != 0;
+    if (!nz) return fail(c, SPGG_E_STATE, "MT19937 jump polynomial unavailable");
+  }
+  return hip_check(c, hipMemcpy(c->d_polys, polys.data(), polys.size() * 4, hipMemcpyHostToDevice),
+                   "hipMemcpy(mt polys)");
 }
 
+// Chained generator (chains > 1): before chunk 0, every chain's window is seeded with the
+// window at iteration 1's first word and jumped by (its chain index) x per_chain iterations,
+// one jump level per bit of the index; after chunk q's generation, chains >= 1 jump one
+// chunk ahead (chain 0 continues from chunk q's last chain: key_out).
 void enqueue_gen_chunk(spgg_ctx* c, int q) {
   const int K = c->gen_chunk;
   const int t0 = q * K + 1, t1 = std::min((q + 1) * K, c->cfg.iterations);
+  const int J = c->jump_levels, R = c->cfg.n_rep;
   if (q >= 2) (void)hipStreamWaitEvent(c->gen_stream, c->step_done[q & 1], 0);
-  launch_gen(c, t0, t1, 1, c->gen_stream);
+  if (c->chains > 1 && q == 0) {
+    spgg_mt::launch_seed(c->buf.mt_state, c->d_run_pos0, c->d_parts[J & 1], R, c->chains, c->gen_stream);
+    for (int j = 0; j < J; ++j)
+      spgg_mt::launch_jump(c->d_parts[(J - j) & 1], c->d_parts[(J - j - 1) & 1], c->d_polys + (size_t)j * 624, R,
+                           c->chains, j, nullptr, c->gen_stream);
+  }
+  launch_gen(c, t0, t1, 1, c->gen_stream, c->chains > 1 ? q : -1);
   (void)hipEventRecord(c->gen_done[q & 1], c->gen_stream);
+  if (c->chains > 1 && t1 < c->cfg.iterations)
+    spgg_mt::launch_jump(c->d_parts[q & 1], c->d_parts[(q + 1) & 1], c->d_polys + (size_t)J * 624, R, c->chains, -1,
+                         c->buf.stop_iter, c->gen_stream);
   c->gen_upto = t1;
 }
 
@@ -2276,12 +2396,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->cfg = *cfg;
   c->n = cfg->L * cfg->L;
   c->apt = apt;
-  // MT19937 pipeline depth (iterations per generator launch): SPGG_MT_CHUNK, default 8
-  if (const char* e = getenv("SPGG_MT_CHUNK")) c->gen_chunk = std::max(1, std::min(256, atoi(e)));
-  {  // a generator launch indexes its words in 32 bits (below 2^31)
-    const long long per_iter = draw_mt_words(c->n, draw_planes(cfg->algorithm));
-    c->gen_chunk = (int)std::max(1LL, std::min((long long)c->gen_chunk, ((1LL << 31) - (1LL << 16)) / per_iter));
-  }
+  if (cfg->rng_mode == SPGG_RNG_MT19937) choose_mt_chains(c);
   c->draw_slots = 2 * c->gen_chunk;
   c->snap_slots = 3 * c->gen_chunk + 1;
   c->draw_words = draw_words_of(c->n, cfg->algorithm);
@@ -2434,8 +2549,9 @@ int spgg_draw_range(spgg_ctx* c, int32_t t0, int32_t t1, void* stream) {
   if (!c) return SPGG_E_ARG;
   if (!c->bound || c->cfg.rng_mode != SPGG_RNG_MT19937)
     return fail(c, SPGG_E_STATE, "spgg_draw needs a bound MT19937 context");
-  if (t0 < 1 || t1 < t0 || t1 > c->cfg.iterations || t1 - t0 + 1 > c->gen_chunk)
-    return fail(c, SPGG_E_ARG, "spgg_draw_range: 1 <= t0 <= t1 <= iterations, t1 - t0 < gen chunk");
+  if (t0 < 1 || t1 < t0 || t1 > c->cfg.iterations || t1 - t0 + 1 > c->gen_chunk ||
+      (long long)(t1 - t0 + 2) * draw_mt_words(c->n, draw_planes(c->cfg.algorithm)) >= (1LL << 31))
+    return fail(c, SPGG_E_ARG, "spgg_draw_range: 1 <= t0 <= t1 <= iterations, t1 - t0 < gen chunk, < 2^31 words");
   launch_gen(c, t0, t1, 0, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_draw launch");
 }
@@ -2477,6 +2593,14 @@ int spgg_draw_layout(const spgg_ctx* c, int32_t* slots, int64_t* words_per_rep, 
   return SPGG_OK;
 }
 
+int spgg_mt_chains(const spgg_ctx* c, int32_t* chains, int32_t* per_chain) {
+  if (!c || !chains || !per_chain) return SPGG_E_ARG;
+  const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
+  *chains = mt ? c->chains : 1;
+  *per_chain = mt ? c->per_chain : 1;
+  return SPGG_OK;
+}
+
 int spgg_set_draw_stream(spgg_ctx* c, void* stream) {
   if (!c) return SPGG_E_ARG;
   if (c->cfg.rng_mode != SPGG_RNG_MT19937) return fail(c, SPGG_E_STATE, "spgg_set_draw_stream: MT19937 only");
@@ -2498,6 +2622,12 @@ int spgg_destroy(spgg_ctx* c) {
       if (c->step_done[i]) (void)hipEventDestroy(c->step_done[i]);
     }
     if (c->gen_idle) (void)hipEventDestroy(c->gen_idle);
+    for (int i = 0; i < 2; ++i) {
+      if (c->d_parts[i]) (void)hipFree(c->d_parts[i]);
+      if (c->d_keybuf[i]) (void)hipFree(c->d_keybuf[i]);
+    }
+    if (c->d_run_pos0) (void)hipFree(c->d_run_pos0);
+    if (c->d_polys) (void)hipFree(c->d_polys);
     if (c->own_gen_stream) (void)hipStreamDestroy(c->gen_stream);
   }
   delete c;

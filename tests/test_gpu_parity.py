@@ -237,6 +237,51 @@ def test_device_mt_multi_iteration_launch(alg, L):
         eng.close()
 
 
+@pytest.mark.parametrize("chains,per,alg", [(4, 5, "qlearning"), (2, 7, "qlearning"), (8, 3, "sarsa"),
+                                             (4, 4, "double_qlearning")])
+def test_mt_chained_generator_vs_oracle(chains, per, alg, monkeypatch):
+    """The chained MT19937 generator (spgg_mt.h: chain c of a chunk starts from a jumped
+    window) over many chunks -- seeding, the log2(chains) jump levels, the per-chunk jumps,
+    chain 0 continuing from the last chain's key -- reproduces the oracle bit for bit,
+    including replicas that absorb mid-chunk (their keys restored from the snapshot ring):
+    the key after flush is the one RandomState holds after the reference's run."""
+    import ctypes
+    from spgg_amd import _lib as C
+    monkeypatch.setenv("SPGG_MT_CHAINS", str(chains))
+    monkeypatch.setenv("SPGG_MT_PER_CHAIN", str(per))
+    L, T = 40, 120
+    reps = [_runner_params(r=0.5, epsilon=0.05, epsilon_decay=0.5, epsilon_min=0.0, seed=1),  # absorbs at 57
+            _runner_params(r=1.0, epsilon=0.1, epsilon_decay=0.5, epsilon_min=0.0, seed=1),   # absorbs at 46
+            _runner_params(r=3.0, influence_factor=0.0, seed=5),
+            _runner_params(r=4.2, influence_factor=1.5, seed=6)]
+    eng = BatchEngine(L, T, reps, use_second_order=False, rng="mt19937", algorithm=alg, streams=1)
+    try:
+        got = (ctypes.c_int32(), ctypes.c_int32())
+        C.check(eng.lib.spgg_mt_chains(eng.ctx, ctypes.byref(got[0]), ctypes.byref(got[1])), eng.ctx,
+                "spgg_mt_chains")
+        assert (got[0].value, got[1].value) == (chains, per)
+        eng.run(snapshots=False)
+        hs = eng.histories()
+        for k, p in enumerate(reps):
+            rs = np.random.RandomState(p.seed)
+            op = O.Params(L=L, iterations=T, use_second_order=False, state_representation="reputation",
+                          algorithm=alg, **{a: getattr(p, a) for a in (
+                              "r", "c", "cost", "alpha", "gamma", "epsilon", "epsilon_decay", "epsilon_min",
+                              "influence_factor", "lambda_epsilon", "delta_R_D", "R_min", "R_max",
+                              "reward_weight_payoff", "rep_gain_C")})
+            ds, fin = O.run(op, rs, collect_snapshots=False)
+            Q, R, S = eng.final_state(k)
+            assert np.array_equal(Q, fin["Q"]) and np.array_equal(R, fin["R"]) and np.array_equal(S, fin["S"]), k
+            assert np.array_equal(hs[k]["coop_rate_history"], ds["coop_rate_history"]), k
+            key, pos = eng.mt_state_host(k)
+            st = rs.get_state()
+            assert pos == st[2] and np.array_equal(key, st[1]), k
+        if alg == "qlearning":
+            assert [len(hs[k]["coop_rate_history"]) for k in (0, 1)] == [57, 46]
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("apt", ["1", "max"])
 @pytest.mark.parametrize("L,T,M2", [(200, 150, False), (200, 60, True), (1000, 3, False)])
 def test_full_size_bit_exact(L, T, M2, apt, monkeypatch):

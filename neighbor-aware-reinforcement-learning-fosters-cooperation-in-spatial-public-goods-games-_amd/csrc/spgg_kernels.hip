@@ -1580,7 +1580,7 @@ __host__ __device__ inline int64_t draw_words_of(int n, int alg) {
 }
 
 #ifndef SPGG_GEN_OUT
-#define SPGG_GEN_OUT 7
+#define SPGG_GEN_OUT 3
 #endif
 // Timing-only generator ablations (-DSPGG_GEN_ABLATE=mask; draws are WRONG): 1 = no output
 // work (the output waves only track the frontier), 2 = no recurrence arithmetic
@@ -1679,7 +1679,18 @@ __device__ __forceinline__ uint32_t gen_word_pos(uint32_t k) {
 // is ph.  Word indices are relative to the chain's window (the host keeps a chain below
 // 2^31 words).  skip_stopped: replicas already absorbed are left alone (their draws are
 // never read).
-__global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int t0, int t1, int skip_stopped) {
+// VGPR cap (SPGG_GEN_VGPR): the generator shares CUs with the step kernel, whose 5 waves per
+// SIMD hold 5 x 96 of the 512 VGPRs; a generator wave within the remaining 32 displaces none.
+#ifndef SPGG_GEN_VGPR
+#define SPGG_GEN_VGPR 0
+#endif
+#if SPGG_GEN_VGPR
+#define SPGG_GEN_ATTR __attribute__((amdgpu_num_vgpr(SPGG_GEN_VGPR)))
+#else
+#define SPGG_GEN_ATTR
+#endif
+__global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(GenArgs g, int t0, int t1,
+                                                                               int skip_stopped) {
   __shared__ uint32_t ring[kGenRing];
   __shared__ uint32_t gen_done[kGenNR][64];   // blocks recurrence wave r has completed (per lane)
   __shared__ uint32_t gen_need[kGenOut][64];  // output wave w reads no word below this (per lane)
@@ -2055,9 +2066,12 @@ constexpr long long kSmallBatchTiles = 128;
 // MT19937 generator layout (spgg_mt_chains).  One chain generates a replica's draws at
 // ~200 ns per 227 words (measured: 119-215 ns with the steps running), i.e. ~W/227*0.2 us
 // per iteration of W words; the steps take ~15 ps per agent of the batch (cfg3: 62 us for
-// 4.2e6 agents), >= ~8 us.  Chains per replica: a power of two with twice the needed rate.
-// A chain covers >= ~1e6 words (a jump costs ~20 us on 8 workgroups), the draw ring
-// (2 chunks) stays <= 96 MB.  Lattices under 4096 words per iteration keep one chain.
+// 4.2e6 agents), >= ~8 us.  Chains per replica: a power of two with 4x the needed rate; a
+// chain covers >= ~1e6 words (a jump costs ~20 us on 8 workgroups) and a chunk >= 128
+// iterations (cfg3, 105 x L=200, us/step by chains x iterations per chain: 16x4 86.0,
+// 32x2 96.4 -- 64-iteration chunks; 16x9 71.2, 8x18 72.7, 32x4 74.0, 64x2 74.8 -- 128-144;
+// profiles/r03/mt_chain_layouts.txt); the draw ring (2 chunks) stays <= 512 MB.  Lattices
+// under 4096 words per iteration keep one chain.
 void choose_mt_chains(spgg_ctx* c) {
   const spgg_config& cfg = c->cfg;
   const long long W = draw_mt_words(c->n, draw_planes(cfg.algorithm));
@@ -2066,11 +2080,12 @@ void choose_mt_chains(spgg_ctx* c) {
     const double gen_ns = W / 227.0 * 200.0;
     const long long batch = cfg.batch_reps > 0 ? cfg.batch_reps : cfg.n_rep;
     const double step_ns = std::max(8000.0, (double)batch * c->n * 0.015);
-    const double need = 2.0 * gen_ns / step_ns;
+    const double need = 4.0 * gen_ns / step_ns;
     while (chains < 256 && chains < need) chains *= 2;
-    if (chains > 1) per = (int)std::max(1LL, (1000000 + W - 1) / W);
+    if (chains > 1)
+      per = (int)std::max((1000000 + W - 1) / W, (long long)((128 + chains - 1) / chains));
     const double rec = draw_words_of(c->n, cfg.algorithm) * 4.0 * cfg.n_rep;  // bytes per iteration
-    while (chains > 1 && 2.0 * chains * per * rec > 96e6) {
+    while (chains > 1 && 2.0 * chains * per * rec > 512e6) {
       if (per > 1) per = std::max(1, per / 2);
       else chains /= 2;
     }

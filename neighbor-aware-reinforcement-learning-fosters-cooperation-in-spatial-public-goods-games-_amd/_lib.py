@@ -35,7 +35,7 @@ EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
             "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range",
-            "spgg_mt_chains", "spgg_mt_jump_poly")
+            "spgg_mt_chains", "spgg_mt_jump_poly", "spgg_stream_create", "spgg_stream_destroy")
 
 
 class Config(ctypes.Structure):
@@ -125,6 +125,10 @@ def load(path: str | None = None):
         lib.spgg_mt_chains.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         lib.spgg_mt_jump_poly.restype = ctypes.c_int
         lib.spgg_mt_jump_poly.argtypes = [ctypes.c_int64, vp]
+        lib.spgg_stream_create.restype = ctypes.c_int
+        lib.spgg_stream_create.argtypes = [i32, ctypes.POINTER(vp)]
+        lib.spgg_stream_destroy.restype = ctypes.c_int
+        lib.spgg_stream_destroy.argtypes = [vp]
         lib.spgg_set_draw_stream.restype = ctypes.c_int
         lib.spgg_set_draw_stream.argtypes = [vp, vp]
         lib.spgg_build_id.restype = ctypes.c_char_p

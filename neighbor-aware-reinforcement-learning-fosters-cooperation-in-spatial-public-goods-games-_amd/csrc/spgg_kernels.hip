@@ -1562,6 +1562,10 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 
 using spgg_mt::mt_next;
 
+// bit 0 of mt_temper(y) as a function of y: y0 ^ y3 ^ y14 ^ y18 ^ y22 ^ y29 (the tempering
+// shifts and masks of mt_temper composed; tests/test_mt_jump_cpu.py checks it on numpy)
+constexpr uint32_t kTemperBit0 = 0x20444009u;
+
 // Draw program of one iteration, in the reference's order: plane i is rand(L,L)
 // compared with a threshold (2 words per value, i even) or randint(0,2,(L,L))
 // (1 word, i odd).
@@ -1767,7 +1771,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     // key after iteration t (words [mb, mb+624) and pos), to the snapshot ring; then the next
     auto retire = [&]() {
       uint32_t* sn = g.snap + (size_t)(t % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
-#pragma unroll
+#pragma unroll 1
       for (int m = 0; m < 10; ++m) {
         const uint32_t i = lane + 64 * m;
         if (i < 624) sn[i] = ring[gen_word_pos(mb + i)];
@@ -1885,13 +1889,16 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
         const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
         const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
         bool flag;
-        if (dbl) {  // rand() < thr: ((a>>5) * 2^26 + (b>>6)) / 2^53 < thr as a 53-bit integer compare
+        if (dbl) {  // rand() < thr: ((a>>5) * 2^26 + (b>>6)) / 2^53 < thr as a 53-bit integer compare,
+                    // decided by a alone unless its 27 bits equal thr's (p = 2^-27: b read only then)
+          const uint64_t th = (g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr;
+          const uint32_t th_hi = (uint32_t)(th >> 26), th_lo = (uint32_t)th & ((1u << 26) - 1u);
           const uint32_t o = o0 + 2 * lane;
-          const uint32_t a = mt_temper(rb[gen_spill(o)]), b = mt_temper(rb[gen_spill(o + 1)]);
-          const uint64_t v = ((uint64_t)(a >> 5) << 26) | (b >> 6);
-          flag = v < ((g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr);
-        } else {    // randint(0, 2) = the word's low bit
-          flag = (mt_temper(rb[gen_spill(o0 + lane)]) & 1u) != 0;
+          const uint32_t ah = mt_temper(rb[gen_spill(o)]) >> 5;
+          flag = ah < th_hi;
+          if (ah == th_hi) flag = (mt_temper(rb[gen_spill(o + 1)]) >> 6) < th_lo;
+        } else {    // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
+          flag = (__builtin_popcount(rb[gen_spill(o0 + lane)] & kTemperBit0) & 1) != 0;
         }
         const uint64_t bits = __ballot(flag && lane < cnt);  // (lanes past n read stale words)
         if (lane < 2) rec_out[(2 * c + lane) * planes + p] = (uint32_t)(lane ? bits >> 32 : bits);
@@ -2281,6 +2288,34 @@ void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t
                      skip_stopped);
 }
 
+// A stream for the library's generator (gen) or the caller's replica groups (spgg_stream_create).
+// HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4), and streams that share
+// one are serialised; SPGG_STREAM_MODE: 0 = hipStreamCreateWithFlags, 1 = greatest priority,
+// 2 = a CU mask of every CU (a queue of its own), 3 = CU-masked and partitioned: the
+// generator on every SPGG_GEN_CU_STRIDE-th CU (default 8: 32 of 256), the groups on the rest.
+hipError_t make_stream(hipStream_t* s, bool gen) {
+  const char* e = getenv("SPGG_STREAM_MODE");
+  const int mode = e ? atoi(e) : 0;
+  if (mode == 1) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, gen ? hi : lo);
+  } else if (mode == 2 || mode == 3) {
+    int dev = 0, cus = 0;
+    hipError_t r = hipGetDevice(&dev);
+    if (r == hipSuccess) r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (r == hipSuccess && cus > 0) {
+      const char* st = getenv("SPGG_GEN_CU_STRIDE");
+      const int stride = std::max(2, st ? atoi(st) : 8);
+      std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+      for (int i = 0; i < cus; ++i)
+        if (mode == 2 || ((i % stride == 0) == gen)) mask[i / 32] |= 1u << (i % 32);
+      return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 // MT19937 pipeline: generation of chunk q (iterations q*K+1 .. (q+1)*K) waits for the steps
 // of chunk q-2 (whose ring slots it reuses) and is enqueued when chunk q-1 starts, so it
 // overlaps the steps of chunk q-1; the steps of chunk q wait for it.
@@ -2288,7 +2323,7 @@ int mt_lazy_init(spgg_ctx* c) {
   if (c->gen_done[0]) return SPGG_OK;
   int rc = SPGG_OK;
   if (!c->gen_stream) {
-    rc = hip_check(c, hipStreamCreateWithFlags(&c->gen_stream, hipStreamNonBlocking), "hipStreamCreate(gen)");
+    rc = hip_check(c, make_stream(&c->gen_stream, true), "hipStreamCreate(gen)");
     if (rc) return rc;
     c->own_gen_stream = true;
   }
@@ -2614,6 +2649,21 @@ int spgg_mt_chains(const spgg_ctx* c, int32_t* chains, int32_t* per_chain) {
   *chains = mt ? c->chains : 1;
   *per_chain = mt ? c->per_chain : 1;
   return SPGG_OK;
+}
+
+int spgg_stream_create(int32_t device, void** stream) {
+  if (!stream) return SPGG_E_ARG;
+  *stream = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return SPGG_E_HIP;
+  hipStream_t s = nullptr;
+  if (make_stream(&s, false) != hipSuccess) return SPGG_E_HIP;
+  *stream = s;
+  return SPGG_OK;
+}
+
+int spgg_stream_destroy(void* stream) {
+  if (!stream) return SPGG_E_ARG;
+  return hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)) == hipSuccess ? SPGG_OK : SPGG_E_HIP;
 }
 
 int spgg_set_draw_stream(spgg_ctx* c, void* stream) {

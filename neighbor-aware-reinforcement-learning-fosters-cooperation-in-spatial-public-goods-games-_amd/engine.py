@@ -312,8 +312,16 @@ class BatchEngine:
         for k, p in enumerate(params):
             p.stream_id = self.replica_offset + k
         self.groups = []
+        self._own_streams = []
         if self.G == 1:
             streams = [torch.cuda.current_stream(self.dev)]
+        elif os.environ.get("SPGG_OWN_STREAMS", "0") == "1":
+            # streams made by the library (spgg_stream_create, SPGG_STREAM_MODE), not torch's pool
+            for _ in range(self.resident):
+                h = ctypes.c_void_p()
+                C.check(self.lib.spgg_stream_create(self.dev.index, ctypes.byref(h)), None, "spgg_stream_create")
+                self._own_streams.append(h.value)
+            streams = [torch.cuda.ExternalStream(h, device=self.dev) for h in self._own_streams]
         else:
             streams = [torch.cuda.Stream(self.dev) for _ in range(self.resident)]
         bounds = np.linspace(0, self.R, self.G + 1).round().astype(int)
@@ -412,6 +420,12 @@ class BatchEngine:
                 g["ctx"] = None
         self.groups = []
         self.ctx = None
+        if getattr(self, "_own_streams", None):
+            torch.cuda.synchronize(self.dev)
+            self.streams = []
+            for h in self._own_streams:
+                self.lib.spgg_stream_destroy(h)
+            self._own_streams = []
 
     def __del__(self):
         try:

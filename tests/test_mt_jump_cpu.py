@@ -99,3 +99,14 @@ def test_powers_compose():
     y = _stream(w1, D2 + 624)
     w2 = np.bitwise_xor.reduce(y[1 + _poly(D2 - 1)[:, None] + j[None, :]], axis=0)
     assert np.array_equal(w2, x[D1 + D2: D1 + D2 + 624])
+
+
+def test_tempered_low_bit_is_a_parity_of_raw_bits():
+    """randint(0, 2) is the tempered word's bit 0; the generator computes it as the parity of
+    raw bits 0, 3, 14, 18, 22, 29 (spgg_kernels.hip kTemperBit0)."""
+    y = np.random.RandomState(0).randint(0, 2 ** 32, size=200_000, dtype=np.uint32)
+    z = y & np.uint32(0x20444009)
+    par = np.zeros_like(z)
+    for b in range(32):
+        par ^= (z >> np.uint32(b)) & np.uint32(1)
+    assert np.array_equal(_temper(y) & np.uint32(1), par)

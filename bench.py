@@ -173,6 +173,8 @@ def main():
                     help="also time the config's whole run (iterations; -1: BASELINE.json's, when it "
                          "takes under a minute at the measured step time; 0: off)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-mt", action="store_true",
+                    help="skip the MT19937 (product-path) window reported beside a Philox line")
     args = ap.parse_args()
 
     import numpy as np
@@ -197,61 +199,73 @@ def main():
                 for i in range(args.replicas)]
         desc += f" [experiment: {args.replicas} replicas]"
     K, W = args.steps, args.warmup
-    T = K + W
-    eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=args.rng,
-                      streams=args.streams, replica_offset=rank * len(reps))
+
+    def window(rng):
+        """W untimed + K timed iterations of a fresh engine in `rng` mode (barrier +
+        synchronize on both sides; max over ranks): the executed agent-steps, times, layout."""
+        eng = BatchEngine(L, K + W, reps, use_second_order=M2, state_representation=state, rng=rng,
+                          streams=args.streams, replica_offset=rank * len(reps))
+        mt_layout = None
+        if rng == "mt19937":  # the draw generator's chains (spgg_mt_chains)
+            import ctypes
+            ch, per = ctypes.c_int32(), ctypes.c_int32()
+            eng.lib.spgg_mt_chains(eng.ctx, ctypes.byref(ch), ctypes.byref(per))
+            mt_layout = {"chains_per_replica": ch.value, "iterations_per_chain": per.value}
+        eng.step(W)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        eng.step(K)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        dev_ms = ev0.elapsed_time(ev1)
+        stop = eng.stop_iter.cpu().numpy()
+        # executed iterations in the timed window [W+1, W+K] per replica
+        last = np.where(stop == 0, W + K, stop - 1)
+        executed = np.clip(last - W, 0, K)
+        agent_steps = float(executed.sum()) * L * L
+        ncoop = eng.stats_folded()[:, :, 0].cpu().numpy()  # SPGG_ST_NCOOP per iteration slot
+        coop = np.array([ncoop[k, int(last[k]) + 1] / (L * L) for k in range(len(reps))])
+        tot = torch.tensor([agent_steps, wall], dtype=torch.float64, device=torch.device("cuda", local))
+        if dist:
+            s_ = tot[:1].clone()
+            dist.all_reduce(s_, op=dist.ReduceOp.SUM)
+            w_ = tot[1:].clone()
+            dist.all_reduce(w_, op=dist.ReduceOp.MAX)
+            agent_steps_all, wall_max = float(s_.item()), float(w_.item())
+        else:
+            agent_steps_all, wall_max = agent_steps, wall
+        out = dict(agent_steps=agent_steps, agent_steps_all=agent_steps_all, wall=wall, wall_max=wall_max,
+                   dev_ms=dev_ms, coop=coop, mt_layout=mt_layout, resident=eng.resident, groups=eng.G,
+                   waves=eng.waves)
+        eng.close()   # before the next engine, the full run and the CPU baseline's worker processes
+        return out
+
     n_agents = len(reps) * L * L
-    mt_layout = None
-    if args.rng == "mt19937":  # the draw generator's chains (spgg_mt_chains)
-        import ctypes
-        ch, per = ctypes.c_int32(), ctypes.c_int32()
-        eng.lib.spgg_mt_chains(eng.ctx, ctypes.byref(ch), ctypes.byref(per))
-        mt_layout = {"chains_per_replica": ch.value, "iterations_per_chain": per.value}
-
-    eng.step(W)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    eng.step(K)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)
-    stop = eng.stop_iter.cpu().numpy()
-    # executed iterations in the timed window [W+1, W+K] per replica
-    last = np.where(stop == 0, W + K, stop - 1)
-    executed = np.clip(last - W, 0, K)
-    agent_steps = float(executed.sum()) * L * L
-
+    main_w = window(args.rng)
+    agent_steps, wall, dev_ms = main_w["agent_steps"], main_w["wall"], main_w["dev_ms"]
+    agent_steps_all, wall_max, mt_layout = main_w["agent_steps_all"], main_w["wall_max"], main_w["mt_layout"]
     # final cooperation-rate gather over RCCL (the path's only collective)
-    ncoop = eng.stats_folded()[:, :, 0].cpu().numpy()  # SPGG_ST_NCOOP per iteration slot
-    coop = torch.from_numpy(np.array([ncoop[k, int(last[k]) + 1] / (L * L) for k in range(len(reps))]))
-    coop = coop.to(torch.device("cuda", local))
-    tot = torch.tensor([agent_steps, wall], dtype=torch.float64, device=coop.device)
+    coop = torch.from_numpy(main_w["coop"]).to(torch.device("cuda", local))
     if dist:
         gathered = [torch.empty_like(coop) for _ in range(world)]
         dist.all_gather(gathered, coop)
-        s = tot[:1].clone()
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        w = tot[1:].clone()
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        agent_steps_all, wall_max = float(s.item()), float(w.item())
-    else:
-        agent_steps_all, wall_max = agent_steps, wall
     value = agent_steps_all / wall_max
     per_step_dev_s = dev_ms / 1e3 / K
     step_agents = agent_steps / K
     achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
     achieved_wall = ALGO_BYTES_PER_AGENT_STEP * agent_steps / wall / 1e9
-    resident, groups, waves = eng.resident, eng.G, eng.waves
-    eng.close()   # before the full run and the CPU baseline's worker processes
+    resident, groups, waves = main_w["resident"], main_w["groups"], main_w["waves"]
+    # the drop-in SPGG.run / sweep path: the device MT19937 stream, bit-identical to the reference
+    mt_w = window("mt19937") if args.rng == "philox" and not args.no_mt else None
 
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "r03", f"traffic_{args.config}.json")
@@ -287,8 +301,17 @@ def main():
         T_full = FULL_RUN_ITERS.get(args.config, 0) if args.full_run < 0 else args.full_run
         if args.full_run < 0 and wall_max / K * T_full > 60.0:
             T_full = 0
+        if mt_w:
+            line["mt19937"] = {
+                "value": mt_w["agent_steps_all"] / mt_w["wall_max"], "unit": "agent-steps/s",
+                "ms_per_step": mt_w["wall_max"] * 1e3 / K, "mt_chains": mt_w["mt_layout"],
+                "note": "the same K/W window with the device MT19937 stream (bit-identical to the reference's "
+                        "numpy draws; what SPGG.run and the sweep use): spgg_step_kernel + the chained "
+                        "draw generator (spgg_mt_gen_kernel, mt_jump_kernel) on its own stream"}
         if world == 1 and T_full > 0:
             line["full_run"] = full_run(L, M2, state, reps, args.rng, args.streams, T_full, 0)
+            if mt_w:
+                line["mt19937"]["full_run"] = full_run(L, M2, state, reps, "mt19937", args.streams, T_full, 0)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(L, M2, state, reps, args.cpu_budget)
         print(json.dumps(line), flush=True)

@@ -1594,6 +1594,9 @@ __host__ __device__ inline int64_t draw_words_of(int n, int alg) {
 #ifndef SPGG_GEN_NR
 #define SPGG_GEN_NR 1
 #endif
+#ifndef SPGG_GEN_SETPRIO  // wave priority of the recurrence wave(s)
+#define SPGG_GEN_SETPRIO 3
+#endif
 // Blocks between two progress publications of a lone recurrence wave (each publication waits
 // for the wave's LDS writes: one exposed LDS round trip per period); two recurrence waves
 // depend on each other's previous block and publish every block.
@@ -1747,7 +1750,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
   }
   if (wave < kGenNR) {
     // ---- the recurrence: wave r owns slots [r*kGenSPW, (r+1)*kGenSPW) of every block ------
-    __builtin_amdgcn_s_setprio(3);  // the critical path
+    __builtin_amdgcn_s_setprio(SPGG_GEN_SETPRIO);  // the critical path
     const int r = wave;
     uint32_t prev[kGenSPW], ca[kGenSPW], cb[kGenSPW];
     uint32_t *wp[kGenSPW], *pa[kGenSPW], *pb[kGenSPW];  // lane addresses: own word, its two operands
@@ -2291,11 +2294,11 @@ void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t
 // A stream for the library's generator (gen) or the caller's replica groups (spgg_stream_create).
 // HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4), and streams that share
 // one are serialised; SPGG_STREAM_MODE: 0 = hipStreamCreateWithFlags, 1 = greatest priority,
-// 2 = a CU mask of every CU (a queue of its own), 3 = CU-masked and partitioned: the
+// 2 (default) = a CU mask of every CU (a queue of its own), 3 = CU-masked and partitioned: the
 // generator on every SPGG_GEN_CU_STRIDE-th CU (default 8: 32 of 256), the groups on the rest.
 hipError_t make_stream(hipStream_t* s, bool gen) {
   const char* e = getenv("SPGG_STREAM_MODE");
-  const int mode = e ? atoi(e) : 0;
+  const int mode = e ? atoi(e) : 2;  // (cfg3 MT19937 whole run: mode 0 95.4 us/iter, 2 88.8)
   if (mode == 1) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
@@ -2550,14 +2553,17 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
   }
   if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
   const int K = c->gen_chunk, T = c->cfg.iterations;
+  // timing-only knobs (results are WRONG): SPGG_TIMING=1 skips the step launches (generator
+  // alone), =2 the generator launches (steps on stale draws)
+  static const int timing = getenv("SPGG_TIMING") ? atoi(getenv("SPGG_TIMING")) : 0;
   for (int t = t0; t < t0 + n_steps; ++t) {
     if (mt) {
       const int q = (t - 1) / K;
       // this chunk and the next one enqueued (the next overlaps this chunk's steps)
-      while (c->gen_upto < std::min(T, (q + 2) * K)) enqueue_gen_chunk(c, c->gen_upto / K);
-      if (t == q * K + 1 || t == t0) (void)hipStreamWaitEvent(s, c->gen_done[q & 1], 0);
+      while (timing != 2 && c->gen_upto < std::min(T, (q + 2) * K)) enqueue_gen_chunk(c, c->gen_upto / K);
+      if (timing != 2 && (t == q * K + 1 || t == t0)) (void)hipStreamWaitEvent(s, c->gen_done[q & 1], 0);
     }
-    launch_step(c, t, 0, s);
+    if (timing != 1) launch_step(c, t, 0, s);
     if (mt && (t % K == 0 || t == T)) (void)hipEventRecord(c->step_done[((t - 1) / K) & 1], s);
   }
   return hip_check(c, hipGetLastError(), "spgg_step launch");

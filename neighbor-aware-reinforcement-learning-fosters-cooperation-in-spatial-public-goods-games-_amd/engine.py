@@ -315,8 +315,11 @@ class BatchEngine:
         self._own_streams = []
         if self.G == 1:
             streams = [torch.cuda.current_stream(self.dev)]
-        elif os.environ.get("SPGG_OWN_STREAMS", "0") == "1":
-            # streams made by the library (spgg_stream_create, SPGG_STREAM_MODE), not torch's pool
+        elif os.environ.get("SPGG_OWN_STREAMS", "1") == "1":
+            # streams made by the library (spgg_stream_create, SPGG_STREAM_MODE), not torch's pool:
+            # torch's pool streams share HIP's few hardware queues with every earlier user, and
+            # two streams on one queue run serialised (cfg3, a second engine in the process:
+            # 80-82 us/iter on pool streams, 58.5-59 on the library's; profiles/r03/streams.txt)
             for _ in range(self.resident):
                 h = ctypes.c_void_p()
                 C.check(self.lib.spgg_stream_create(self.dev.index, ctypes.byref(h)), None, "spgg_stream_create")

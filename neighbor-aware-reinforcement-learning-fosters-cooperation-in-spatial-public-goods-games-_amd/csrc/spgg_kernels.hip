@@ -175,8 +175,13 @@ namespace {
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_DR, off_DP, bytes;
 };
+
+// Staged draw bits (MT19937 / inject, compile-time-width tiles): per region row, the draw-record
+// words (planes 0, 1) of kDrawSlots 32-agent groups -- 3 from the row's first cell (x0 - HA),
+// 3 from column 0 (the cells past the periodic wrap) -- and, repacked, the row's 64 region cells.
+constexpr int kDrawSlots = 6;
 
 // Pitch of the plus-count plane: one 64-lane wave row per region row.
 constexpr int kPcPitch = 64;
@@ -187,7 +192,8 @@ constexpr int kPcPitch = 64;
 // dword_rows (compile-time-width kernels): every plane has one dword-aligned
 // pitch wide enough for a window staged as aligned dwords (window column j at
 // plane column j + its 0..3-byte misalignment).
-__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, int rsz, bool dword_rows = false) {
+__host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, int rsz, bool dword_rows = false,
+                                                bool draws = false) {
   LdsLayout l;
   l.sw = tw + 2 * HS; l.sh = th + 2 * HS;
   l.aw = tw + 2 * HA; l.ah = th + 2 * HA;
@@ -201,6 +207,9 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_D = off;    off += ((l.sw * l.sh + kPcPitch + 15) / 16) * 16;  // + slack: full-wave row reads
   l.off_A = off;    off += ((na + 15) / 16) * 16;
   l.off_PC = off;   off += (l.ah + 2) * kPcPitch;
+  off = (off + 15) / 16 * 16;
+  l.off_DR = off;   off += draws ? l.ah * kDrawSlots * 2 * 4 : 0;
+  l.off_DP = off;   off += draws ? l.ah * 2 * 2 * 4 : 0;
   l.bytes = off;
   return l;
 }
@@ -556,6 +565,13 @@ __device__ __forceinline__ void draw_pair(const TileArgs& a, int rep, int g, int
   }
 }
 
+// Draw pair 0 of region cell (ry, rx) from the staged bits (spgg_step_kernel, DSTAGE).
+__device__ __forceinline__ void staged_draw(const uint2* sDP, int ry, int rx, int* ex, int* rbt) {
+  const uint2 w = sDP[ry * 2 + (rx >> 5)];
+  *ex = (int)((w.x >> (rx & 31)) & 1u);
+  *rbt = (int)((w.y >> (rx & 31)) & 1u);
+}
+
 // Double-Q's table choice (rand < 0.5, algorithms.py:302): plane 2, or Philox pair 1.
 template <int RNG>
 __device__ __forceinline__ int draw_table1(const TileArgs& a, int rep, int g, int t, uint32_t key) {
@@ -780,7 +796,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const int th = min(a.TH, L - y0), tw = TWC ? TWC : min(a.TW, L - x0);
   // LDS pitches from the full tile width (constants when TWC > 0); edge tiles
   // use the top-left part of each region
-  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HA, (int)sizeof(RT), true)
+  // draw bits staged through LDS (one load round trip with the windows) instead of a record
+  // load per agent at the point of use (MT19937 steps 8 us slower than Philox before this)
+  constexpr bool DSTAGE = RNG != SPGG_RNG_PHILOX && TWC > 0;
+  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HA, (int)sizeof(RT), true, DSTAGE)
                            : lds_layout(tw, th, HS, HA, (int)sizeof(RT));
   double* tab = reinterpret_cast<double*>(smem);
   double* red = tab + 12;
@@ -791,6 +810,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint8_t* sD = smem + ly.off_D;
   uint8_t* sA = smem + ly.off_A;
   uint8_t* sPC = smem + ly.off_PC;
+  uint32_t* sDR = reinterpret_cast<uint32_t*>(smem + ly.off_DR);  // [row][slot][plane]
+  uint2* sDP = reinterpret_cast<uint2*>(smem + ly.off_DP);         // [row][half] (plane 0, plane 1)
   // this replica's arrays: scalar bases, 32-bit element offsets (at())
   const size_t rb = (size_t)rep * n;
   double* Qr = a.Q + rb * QW;
@@ -911,6 +932,20 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : *at(atdr, g);  // 256: atd traffic floor probe
     }
   }
+  // draw-record words of the region rows (DSTAGE): row ry, slot sl: 32-agent group
+  // (gy*L + (sl < 3 ? xA : 0)) / 32 + sl % 3, planes 0 and 1 (adjacent words)
+  const uint32_t xA = wrap_once(x0 - HA, L);        // the region's first column
+  const int a_len = min(aw, L - (int)xA);           // region cells before the periodic wrap
+  uint32_t dw0 = 0, dw1 = 0;
+  if constexpr (DSTAGE) {
+    const int i = min(tid, ah * kDrawSlots - 1), ry = i / kDrawSlots, sl = i - ry * kDrawSlots;
+    const uint32_t gy = wrap_once(y0 - HA + ry, L);
+    const uint32_t grp = min((gy * (uint32_t)L + (sl < 3 ? xA : 0u)) / 32u + (uint32_t)(sl % 3),
+                             (uint32_t)(a.draw_words / a.planes - 1));
+    const uint32_t wi = (uint32_t)rep * a.draw_words + grp * a.planes;
+    dw0 = *at(a.draws, wi);
+    dw1 = *at(a.draws, wi + 1);
+  }
   // replica state (scalar loads)
   const int st = a.stop_iter[rep];
   const bool dead = st != 0 && st < t;  // absorbed before t: nothing to do
@@ -966,6 +1001,12 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     stage_region<JSF>(sS, ly.sw, Sin, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny, sD);
     if (!AS) stage_region<JRF>(sR, ly.aw, Rin, ah, aw, y0 - HA, x0 - HA, L, tiny);
   }
+  if constexpr (DSTAGE) {
+    if (tid < ah * kDrawSlots) {
+      sDR[tid * 2] = dw0;
+      sDR[tid * 2 + 1] = dw1;
+    }
+  }
   if (dead) return;  // workgroup-uniform; no vector load is outstanding here
   if (stop_now && tile == 0 && tid == 0) a.stop_iter[rep] = t;
   // border records of this thread's ring cells: in flight during phases 1a / 1b
@@ -997,6 +1038,33 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (!fin_only) {
     if constexpr (TWC > 0) build_plus_counts_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPC, sD, ly.sw, ah + 2, soffS);
     else build_plus_counts(sPC, sDv, ly.sw, ah + 2);
+  }
+  // draw bits repacked to the region (DSTAGE): word (row ry, half h) holds cells rx = 32h ..
+  // 32h+31 -- bit offA + rx of the row's first three groups for rx < a_len, bit offB + rx -
+  // a_len of the three from column 0 past the wrap (read in phases 1b / 1c, after the barrier)
+  if constexpr (DSTAGE) {
+    if (!fin_only && tid < ah * 2) {
+      const int ry = tid >> 1, r0 = (tid & 1) * 32;
+      const uint32_t gyL = wrap_once(y0 - HA + ry, L) * (uint32_t)L;
+      const int offA = (int)((gyL + xA) & 31u), offB = (int)(gyL & 31u);
+      const uint32_t* W = sDR + ry * kDrawSlots * 2;
+      auto bits32 = [&](int slot0, int bitpos, int p) {  // 32 bits from bitpos of slots slot0..slot0+2
+        const int w = bitpos >> 5;
+        const uint32_t lo = W[(slot0 + min(w, 2)) * 2 + p], hi = W[(slot0 + min(w + 1, 2)) * 2 + p];
+        return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(bitpos & 31));
+      };
+      uint32_t out[2] = {0u, 0u};
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        if (r0 < a_len) out[p] = bits32(0, offA + r0, p);
+        if (a_len < r0 + 32) {  // cells from the wrapped part
+          const int rs = max(r0, a_len), sh = rs - r0;
+          const uint32_t mB = ~0u << sh;
+          out[p] = (out[p] & ~mB) | ((bits32(3, offB + rs - a_len, p) << sh) & mB);
+        }
+      }
+      sDP[ry * 2 + (r0 >> 5)] = make_uint2(out[0], out[1]);
+    }
   }
 
   // ---- phase 1a: finalize iteration t-1 for owned agents -----------------
@@ -1119,6 +1187,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                                                             // R_t (S_t bit 4; iteration 1: the prologue)
       int ex, rbt;                                          // algorithms.py:105-109
       if constexpr (PAIRED) philox_decide(pbits[u], eps53, &ex, &rbt);
+      else if constexpr (DSTAGE) staged_draw(sDP, r + HA, c + HA, &ex, &rbt);
       else draw_pair<RNG>(a, rep, agent_of(rc[u]), t, pkey, eps53, 0, &ex, &rbt);
       double qs0, qs1;
       select_row<QB>(q[u], qb[u], so, &qs0, &qs1);
@@ -1180,7 +1249,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const double P = payoff_pc(sPC, ay, ax, tab + ((b & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp);
       const RVal<RQ> r_t = AS ? RVal<RQ>(0) : RVal<RQ>(sRv[ay * ly.aw + ax]);
       int ex, rbt;
-      draw_pair<RNG>(a, rep, g, t, pkey, eps53, 0, &ex, &rbt);
+      if constexpr (DSTAGE) staged_draw(sDP, ay, ax, &ex, &rbt);
+      else draw_pair<RNG>(a, rep, g, t, pkey, eps53, 0, &ex, &rbt);
       const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
       const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
       const double rr = act == 0 ? 0.5 : 0.0;
@@ -1914,6 +1984,199 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
   LDS_ST(gen_need[ow][lane], 0xffffffffu);  // done: never blocks the recurrence
 }
 
+// Single-wave chain generator (the default; SPGG_GEN1=0 selects spgg_mt_gen_kernel above).
+// One 64-lane wave per chain and no flags: the recurrence of block b (positions F = 624 + 227 b
+// + 64 s + lane, slots s = 0..3, slot 3 35 lanes) takes x[k-227] from the lane's register of
+// the previous block and x[k-624], x[k-623] from an LDS ring of 1024 words (position k at
+// k & 1023); then the PREVIOUS block is output from its registers -- tempered, thresholded,
+// one __ballot per slot -- so the second word of every rand() pair is already in the ring
+// (read only on a threshold tie, p = 2^-27).  Draw bits are accumulated per plane in scalar
+// registers and stored one 32-bit record word at a time (a vector store from lane 0); key
+// snapshots are written as soon as their 624-word block is generated.  Same arguments, chain
+// layout and outputs as spgg_mt_gen_kernel.
+constexpr int kG1Ring = 1024;
+
+__device__ __forceinline__ uint64_t compress_even_bits(uint64_t x) {  // bits 0, 2, 4, .. -> 0, 1, 2, ..
+  x &= 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+}
+
+__global__ __launch_bounds__(64) void spgg_mt_gen1_kernel(GenArgs g, int t0, int t1, int skip_stopped) {
+  __shared__ uint32_t ring[kG1Ring];
+  const int rep = blockIdx.x / g.chains, ch = blockIdx.x - rep * g.chains, lane = threadIdx.x;
+  bool last_chain;
+  {
+    const int ct0 = t0 + ch * g.per_chain;
+    if (ct0 > t1) return;
+    last_chain = ct0 + g.per_chain - 1 >= t1;
+    t1 = min(t1, ct0 + g.per_chain - 1);
+    t0 = ct0;
+  }
+  if (skip_stopped && g.stop_iter[rep] != 0) return;
+  const int planes = draw_planes(g.alg);
+  const uint32_t W = (uint32_t)draw_mt_words(g.n, planes), n = (uint32_t)g.n;
+  uint32_t ph = 0, pos0;
+  if (ch == 0) {
+    const uint32_t* key = g.key_in + (size_t)rep * 625;
+    for (int i = lane; i < 624; i += 64) ring[i] = key[i];
+    pos0 = key[624];
+    if (t0 == 1) {
+      uint32_t* s0 = g.snap + (size_t)rep * 625;
+      for (int i = lane; i < 625; i += 64) s0[i] = key[i];
+    }
+  } else {
+    const uint32_t* pp = g.parts + (size_t)(rep * g.chains + ch) * spgg_mt::kSplits * 624;
+    for (int i = lane; i < 624; i += 64) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int p = 0; p < spgg_mt::kSplits; ++p) v ^= pp[p * 624 + i];
+      ring[i] = v;
+    }
+    pos0 = 0;
+    ph = (uint32_t)(((uint64_t)g.run_pos0[rep] + (uint64_t)(t0 - 1) * W) % 624u);
+  }
+  pos0 = __builtin_amdgcn_readfirstlane(pos0);
+  auto key_block = [ph](uint32_t E) { return ((E - 1 + ph) / 624) * 624 - ph; };
+  const uint64_t thr_half = u53_threshold(0.5);
+
+  // ---- output cursor (wave-uniform) ----
+  int t_out = t0, p = 0;
+  uint32_t ps = pos0, pe = pos0 + 2 * n;             // plane [ps, pe): rand planes 2n words, randint n
+  uint32_t* rec = g.draws + (size_t)((t_out - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
+  uint64_t thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t_out]);
+  uint64_t acc = 0;                                   // pending draw bits of plane p
+  int acc_n = 0;
+  uint32_t acc_w = 0;                                 // their first draw / 32
+  auto put = [&](uint32_t bits, int cnt) {            // append cnt <= 32 bits
+    if (cnt <= 0) return;
+    bits &= cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u);
+    acc |= (uint64_t)bits << acc_n;
+    acc_n += cnt;
+    if (acc_n >= 32) {
+      if (lane == 0) rec[acc_w * (uint32_t)planes + (uint32_t)p] = (uint32_t)acc;
+      acc >>= 32;
+      acc_n -= 32;
+      ++acc_w;
+    }
+  };
+  auto next_plane = [&]() {                           // flush, then the next plane / iteration
+    if (acc_n > 0 && lane == 0) rec[acc_w * (uint32_t)planes + (uint32_t)p] = (uint32_t)acc;
+    acc = 0;
+    acc_n = 0;
+    acc_w = 0;
+    ps = pe;
+    if (++p == planes) {
+      p = 0;
+      if (++t_out > t1) return;
+      rec = g.draws + (size_t)((t_out - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
+      thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t_out]);
+    }
+    pe = ps + ((p & 1) ? n : 2 * n);
+  };
+  // words of positions P + lane, lane < len: their draw bits
+  auto output = [&](uint32_t P, uint32_t x, int len) {
+    int lo = 0;
+    while (lo < len && t_out <= t1) {
+      if (P + (uint32_t)lo >= pe) {
+        next_plane();
+        continue;
+      }
+      if (P + (uint32_t)lo < ps) {                   // (before the chain's first draw word)
+        lo = (int)min((uint32_t)len, ps - P);
+        continue;
+      }
+      const int hi = (int)min((uint32_t)len, pe - P);
+      const bool in = lane >= lo && lane < hi;
+      const uint32_t off = P - ps;                    // plane offset of lane 0
+      if ((p & 1) == 0) {  // rand() < thr: (a>>5) * 2^26 + (b>>6) < thr, decided by a unless tied
+        const uint64_t th = (g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr;
+        const uint32_t th_hi = (uint32_t)(th >> 26), th_lo = (uint32_t)th & ((1u << 26) - 1u);
+        const bool a_lane = in && ((off + (uint32_t)lane) & 1u) == 0u;
+        const uint32_t ah = mt_temper(x) >> 5;
+        bool flag = ah < th_hi;
+        const bool tie = a_lane && ah == th_hi;
+        if (__ballot(tie))
+          if (tie) flag = (mt_temper(ring[(P + (uint32_t)lane + 1u) & (kG1Ring - 1)]) >> 6) < th_lo;
+        const int f = lo + (int)((off + (uint32_t)lo) & 1u);   // first a-word lane
+        const uint64_t m = __ballot(flag && a_lane);
+        if (hi > f) put((uint32_t)compress_even_bits(m >> f), (hi - f + 1) >> 1);
+      } else {             // randint(0, 2): parity of raw bits 0,3,14,18,22,29
+        const bool flag = (__builtin_popcount(x & kTemperBit0) & 1) != 0;
+        const uint64_t m = __ballot(flag && in) >> lo;
+        const int cnt = hi - lo;
+        put((uint32_t)m, min(cnt, 32));
+        put((uint32_t)(m >> 32), cnt - 32);
+      }
+      lo = hi;
+    }
+  };
+  // ---- key snapshots (slot t % snap_slots = the key after iteration t) ----
+  // (the last chain's key after its last iteration goes to key_out from the same copy: the
+  // ring may advance past that block while the output finishes)
+  int t_ret = t0;
+  uint32_t E = pos0 + W, mb = key_block(E);
+  auto retire_upto = [&](uint32_t frontier) {
+    while (t_ret <= t1 && mb + 624u <= frontier) {
+      uint32_t* sn = g.snap + (size_t)(t_ret % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
+      uint32_t* ko = g.key_out + (size_t)rep * 625;
+      const bool to_key = last_chain && t_ret == t1;
+#pragma unroll 1
+      for (int i = lane; i < 624; i += 64) {
+        const uint32_t v = ring[(mb + (uint32_t)i) & (kG1Ring - 1)];
+        sn[i] = v;
+        if (to_key) ko[i] = v;
+      }
+      if (lane == 0) {
+        sn[624] = E - mb;
+        if (to_key) ko[624] = E - mb;
+      }
+      ++t_ret;
+      E += W;
+      mb = key_block(E);
+    }
+  };
+
+  // ---- block 0, then the window's draws, then block b / output b-1 ----
+  uint32_t prev[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) prev[s] = ring[min(397 + 64 * s + lane, 623)];  // x[624 + j - 227]
+  uint32_t F = 624;
+  auto gen_block = [&]() {
+    uint32_t cur[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t k = F + 64u * s + (uint32_t)lane;
+      cur[s] = mt_next(prev[s], ring[(k - 624u) & (kG1Ring - 1)], ring[(k - 623u) & (kG1Ring - 1)]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (s < 3 || lane < kMtBlock - 192) ring[(F + 64u * s + (uint32_t)lane) & (kG1Ring - 1)] = cur[s];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) prev[s] = cur[s];
+    F += kMtBlock;
+  };
+  uint32_t held[4];
+  gen_block();  // block 0: positions 624 .. 850
+#pragma unroll 1
+  for (uint32_t P = 0; P < 624; P += 64) output(P, ring[min(P + (uint32_t)lane, 623u)], (int)min(64u, 624u - P));
+  retire_upto(F);
+  for (uint32_t guard = 0; (t_out <= t1 || t_ret <= t1) && guard < (1u << 24); ++guard) {
+    const uint32_t Fo = F - kMtBlock;  // the block to output: generated last
+#pragma unroll
+    for (int s = 0; s < 4; ++s) held[s] = prev[s];
+    gen_block();
+    if (t_out <= t1) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) output(Fo + 64u * s, held[s], s < 3 ? 64 : kMtBlock - 192);
+    }
+    retire_upto(F);
+  }
+}
+
 // spgg_flush (MT19937): the key the reference holds after the run -- after the last
 // iteration a replica executed (its absorbing iteration draws nothing) -- from the ring.
 __global__ void spgg_mt_final_kernel(GenArgs g, int t_last) {
@@ -2287,8 +2550,12 @@ GenArgs gen_args(const spgg_ctx* c, int q = -1) {
 
 void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t s, int q = -1) {
   const GenArgs g = gen_args(c, q);
-  hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep * g.chains), dim3(kGenThreads), 0, s, g, t0, t1,
-                     skip_stopped);
+  static const bool gen1 = getenv("SPGG_GEN1") && atoi(getenv("SPGG_GEN1")) != 0;
+  if (gen1)
+    hipLaunchKernelGGL(spgg_mt_gen1_kernel, dim3(c->cfg.n_rep * g.chains), dim3(64), 0, s, g, t0, t1, skip_stopped);
+  else
+    hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep * g.chains), dim3(kGenThreads), 0, s, g, t0, t1,
+                       skip_stopped);
 }
 
 // A stream for the library's generator (gen) or the caller's replica groups (spgg_stream_create).
@@ -2296,13 +2563,17 @@ void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t
 // one are serialised; SPGG_STREAM_MODE: 0 = hipStreamCreateWithFlags, 1 = greatest priority,
 // 2 (default) = a CU mask of every CU (a queue of its own), 3 = CU-masked and partitioned: the
 // generator on every SPGG_GEN_CU_STRIDE-th CU (default 8: 32 of 256), the groups on the rest.
+// The generator's stream (SPGG_GEN_STREAM_MODE, default 0) must be NON-blocking: CU-masked
+// streams are blocking, and every operation on the legacy null stream (torch's default) then
+// waits for the generator's queued chunks -- a host sync every 256 iterations drained the
+// pipeline (cfg2 MT19937 whole run 15.8 vs 10.3 us/iter).
 hipError_t make_stream(hipStream_t* s, bool gen) {
-  const char* e = getenv("SPGG_STREAM_MODE");
-  const int mode = e ? atoi(e) : 2;  // (cfg3 MT19937 whole run: mode 0 95.4 us/iter, 2 88.8)
+  const char* e = getenv(gen ? "SPGG_GEN_STREAM_MODE" : "SPGG_STREAM_MODE");
+  const int mode = e ? atoi(e) : gen ? 0 : 2;
   if (mode == 1) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, gen ? hi : lo);
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, gen ? hi : lo);  // (non-blocking)
   } else if (mode == 2 || mode == 3) {
     int dev = 0, cus = 0;
     hipError_t r = hipGetDevice(&dev);
@@ -2468,7 +2739,9 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   // iteration (a single record of an L=1000 replica took 1000 atomics per address: ~12 us)
   while (c->stripes < 32 && (c->tiles_per_rep + c->stripes - 1) / c->stripes > kTilesPerStripe) c->stripes *= 2;
   const int HA = cfg->second_order ? 2 : 1;
-  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8, twc_of(*cfg, c->TW, c->TH) > 0);
+  const bool twc = twc_of(*cfg, c->TW, c->TH) > 0;
+  const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8, twc,
+                                  twc && cfg->rng_mode != SPGG_RNG_PHILOX);  // (the kernel's DSTAGE)
   c->lds_bytes = (size_t)ly.bytes;
   c->PB = spgg_impl::pub_slots(c->TW, c->TH, HA);
   // stage_region's per-thread register window must cover the S and R halos

@@ -1984,199 +1984,6 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
   LDS_ST(gen_need[ow][lane], 0xffffffffu);  // done: never blocks the recurrence
 }
 
-// Single-wave chain generator (the default; SPGG_GEN1=0 selects spgg_mt_gen_kernel above).
-// One 64-lane wave per chain and no flags: the recurrence of block b (positions F = 624 + 227 b
-// + 64 s + lane, slots s = 0..3, slot 3 35 lanes) takes x[k-227] from the lane's register of
-// the previous block and x[k-624], x[k-623] from an LDS ring of 1024 words (position k at
-// k & 1023); then the PREVIOUS block is output from its registers -- tempered, thresholded,
-// one __ballot per slot -- so the second word of every rand() pair is already in the ring
-// (read only on a threshold tie, p = 2^-27).  Draw bits are accumulated per plane in scalar
-// registers and stored one 32-bit record word at a time (a vector store from lane 0); key
-// snapshots are written as soon as their 624-word block is generated.  Same arguments, chain
-// layout and outputs as spgg_mt_gen_kernel.
-constexpr int kG1Ring = 1024;
-
-__device__ __forceinline__ uint64_t compress_even_bits(uint64_t x) {  // bits 0, 2, 4, .. -> 0, 1, 2, ..
-  x &= 0x5555555555555555ull;
-  x = (x | (x >> 1)) & 0x3333333333333333ull;
-  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-  return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
-}
-
-__global__ __launch_bounds__(64) void spgg_mt_gen1_kernel(GenArgs g, int t0, int t1, int skip_stopped) {
-  __shared__ uint32_t ring[kG1Ring];
-  const int rep = blockIdx.x / g.chains, ch = blockIdx.x - rep * g.chains, lane = threadIdx.x;
-  bool last_chain;
-  {
-    const int ct0 = t0 + ch * g.per_chain;
-    if (ct0 > t1) return;
-    last_chain = ct0 + g.per_chain - 1 >= t1;
-    t1 = min(t1, ct0 + g.per_chain - 1);
-    t0 = ct0;
-  }
-  if (skip_stopped && g.stop_iter[rep] != 0) return;
-  const int planes = draw_planes(g.alg);
-  const uint32_t W = (uint32_t)draw_mt_words(g.n, planes), n = (uint32_t)g.n;
-  uint32_t ph = 0, pos0;
-  if (ch == 0) {
-    const uint32_t* key = g.key_in + (size_t)rep * 625;
-    for (int i = lane; i < 624; i += 64) ring[i] = key[i];
-    pos0 = key[624];
-    if (t0 == 1) {
-      uint32_t* s0 = g.snap + (size_t)rep * 625;
-      for (int i = lane; i < 625; i += 64) s0[i] = key[i];
-    }
-  } else {
-    const uint32_t* pp = g.parts + (size_t)(rep * g.chains + ch) * spgg_mt::kSplits * 624;
-    for (int i = lane; i < 624; i += 64) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int p = 0; p < spgg_mt::kSplits; ++p) v ^= pp[p * 624 + i];
-      ring[i] = v;
-    }
-    pos0 = 0;
-    ph = (uint32_t)(((uint64_t)g.run_pos0[rep] + (uint64_t)(t0 - 1) * W) % 624u);
-  }
-  pos0 = __builtin_amdgcn_readfirstlane(pos0);
-  auto key_block = [ph](uint32_t E) { return ((E - 1 + ph) / 624) * 624 - ph; };
-  const uint64_t thr_half = u53_threshold(0.5);
-
-  // ---- output cursor (wave-uniform) ----
-  int t_out = t0, p = 0;
-  uint32_t ps = pos0, pe = pos0 + 2 * n;             // plane [ps, pe): rand planes 2n words, randint n
-  uint32_t* rec = g.draws + (size_t)((t_out - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
-  uint64_t thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t_out]);
-  uint64_t acc = 0;                                   // pending draw bits of plane p
-  int acc_n = 0;
-  uint32_t acc_w = 0;                                 // their first draw / 32
-  auto put = [&](uint32_t bits, int cnt) {            // append cnt <= 32 bits
-    if (cnt <= 0) return;
-    bits &= cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u);
-    acc |= (uint64_t)bits << acc_n;
-    acc_n += cnt;
-    if (acc_n >= 32) {
-      if (lane == 0) rec[acc_w * (uint32_t)planes + (uint32_t)p] = (uint32_t)acc;
-      acc >>= 32;
-      acc_n -= 32;
-      ++acc_w;
-    }
-  };
-  auto next_plane = [&]() {                           // flush, then the next plane / iteration
-    if (acc_n > 0 && lane == 0) rec[acc_w * (uint32_t)planes + (uint32_t)p] = (uint32_t)acc;
-    acc = 0;
-    acc_n = 0;
-    acc_w = 0;
-    ps = pe;
-    if (++p == planes) {
-      p = 0;
-      if (++t_out > t1) return;
-      rec = g.draws + (size_t)((t_out - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
-      thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t_out]);
-    }
-    pe = ps + ((p & 1) ? n : 2 * n);
-  };
-  // words of positions P + lane, lane < len: their draw bits
-  auto output = [&](uint32_t P, uint32_t x, int len) {
-    int lo = 0;
-    while (lo < len && t_out <= t1) {
-      if (P + (uint32_t)lo >= pe) {
-        next_plane();
-        continue;
-      }
-      if (P + (uint32_t)lo < ps) {                   // (before the chain's first draw word)
-        lo = (int)min((uint32_t)len, ps - P);
-        continue;
-      }
-      const int hi = (int)min((uint32_t)len, pe - P);
-      const bool in = lane >= lo && lane < hi;
-      const uint32_t off = P - ps;                    // plane offset of lane 0
-      if ((p & 1) == 0) {  // rand() < thr: (a>>5) * 2^26 + (b>>6) < thr, decided by a unless tied
-        const uint64_t th = (g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr;
-        const uint32_t th_hi = (uint32_t)(th >> 26), th_lo = (uint32_t)th & ((1u << 26) - 1u);
-        const bool a_lane = in && ((off + (uint32_t)lane) & 1u) == 0u;
-        const uint32_t ah = mt_temper(x) >> 5;
-        bool flag = ah < th_hi;
-        const bool tie = a_lane && ah == th_hi;
-        if (__ballot(tie))
-          if (tie) flag = (mt_temper(ring[(P + (uint32_t)lane + 1u) & (kG1Ring - 1)]) >> 6) < th_lo;
-        const int f = lo + (int)((off + (uint32_t)lo) & 1u);   // first a-word lane
-        const uint64_t m = __ballot(flag && a_lane);
-        if (hi > f) put((uint32_t)compress_even_bits(m >> f), (hi - f + 1) >> 1);
-      } else {             // randint(0, 2): parity of raw bits 0,3,14,18,22,29
-        const bool flag = (__builtin_popcount(x & kTemperBit0) & 1) != 0;
-        const uint64_t m = __ballot(flag && in) >> lo;
-        const int cnt = hi - lo;
-        put((uint32_t)m, min(cnt, 32));
-        put((uint32_t)(m >> 32), cnt - 32);
-      }
-      lo = hi;
-    }
-  };
-  // ---- key snapshots (slot t % snap_slots = the key after iteration t) ----
-  // (the last chain's key after its last iteration goes to key_out from the same copy: the
-  // ring may advance past that block while the output finishes)
-  int t_ret = t0;
-  uint32_t E = pos0 + W, mb = key_block(E);
-  auto retire_upto = [&](uint32_t frontier) {
-    while (t_ret <= t1 && mb + 624u <= frontier) {
-      uint32_t* sn = g.snap + (size_t)(t_ret % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
-      uint32_t* ko = g.key_out + (size_t)rep * 625;
-      const bool to_key = last_chain && t_ret == t1;
-#pragma unroll 1
-      for (int i = lane; i < 624; i += 64) {
-        const uint32_t v = ring[(mb + (uint32_t)i) & (kG1Ring - 1)];
-        sn[i] = v;
-        if (to_key) ko[i] = v;
-      }
-      if (lane == 0) {
-        sn[624] = E - mb;
-        if (to_key) ko[624] = E - mb;
-      }
-      ++t_ret;
-      E += W;
-      mb = key_block(E);
-    }
-  };
-
-  // ---- block 0, then the window's draws, then block b / output b-1 ----
-  uint32_t prev[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) prev[s] = ring[min(397 + 64 * s + lane, 623)];  // x[624 + j - 227]
-  uint32_t F = 624;
-  auto gen_block = [&]() {
-    uint32_t cur[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const uint32_t k = F + 64u * s + (uint32_t)lane;
-      cur[s] = mt_next(prev[s], ring[(k - 624u) & (kG1Ring - 1)], ring[(k - 623u) & (kG1Ring - 1)]);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (s < 3 || lane < kMtBlock - 192) ring[(F + 64u * s + (uint32_t)lane) & (kG1Ring - 1)] = cur[s];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) prev[s] = cur[s];
-    F += kMtBlock;
-  };
-  uint32_t held[4];
-  gen_block();  // block 0: positions 624 .. 850
-#pragma unroll 1
-  for (uint32_t P = 0; P < 624; P += 64) output(P, ring[min(P + (uint32_t)lane, 623u)], (int)min(64u, 624u - P));
-  retire_upto(F);
-  for (uint32_t guard = 0; (t_out <= t1 || t_ret <= t1) && guard < (1u << 24); ++guard) {
-    const uint32_t Fo = F - kMtBlock;  // the block to output: generated last
-#pragma unroll
-    for (int s = 0; s < 4; ++s) held[s] = prev[s];
-    gen_block();
-    if (t_out <= t1) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) output(Fo + 64u * s, held[s], s < 3 ? 64 : kMtBlock - 192);
-    }
-    retire_upto(F);
-  }
-}
-
 // spgg_flush (MT19937): the key the reference holds after the run -- after the last
 // iteration a replica executed (its absorbing iteration draws nothing) -- from the ring.
 __global__ void spgg_mt_final_kernel(GenArgs g, int t_last) {
@@ -2550,12 +2357,8 @@ GenArgs gen_args(const spgg_ctx* c, int q = -1) {
 
 void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t s, int q = -1) {
   const GenArgs g = gen_args(c, q);
-  static const bool gen1 = getenv("SPGG_GEN1") && atoi(getenv("SPGG_GEN1")) != 0;
-  if (gen1)
-    hipLaunchKernelGGL(spgg_mt_gen1_kernel, dim3(c->cfg.n_rep * g.chains), dim3(64), 0, s, g, t0, t1, skip_stopped);
-  else
-    hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep * g.chains), dim3(kGenThreads), 0, s, g, t0, t1,
-                       skip_stopped);
+  hipLaunchKernelGGL(spgg_mt_gen_kernel, dim3(c->cfg.n_rep * g.chains), dim3(kGenThreads), 0, s, g, t0, t1,
+                     skip_stopped);
 }
 
 // A stream for the library's generator (gen) or the caller's replica groups (spgg_stream_create).

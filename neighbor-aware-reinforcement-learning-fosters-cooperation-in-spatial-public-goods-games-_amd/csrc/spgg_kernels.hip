@@ -2366,17 +2366,20 @@ void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t
 // one are serialised; SPGG_STREAM_MODE: 0 = hipStreamCreateWithFlags, 1 = greatest priority,
 // 2 (default) = a CU mask of every CU (a queue of its own), 3 = CU-masked and partitioned: the
 // generator on every SPGG_GEN_CU_STRIDE-th CU (default 8: 32 of 256), the groups on the rest.
-// The generator's stream (SPGG_GEN_STREAM_MODE, default 0) must be NON-blocking: CU-masked
-// streams are blocking, and every operation on the legacy null stream (torch's default) then
-// waits for the generator's queued chunks -- a host sync every 256 iterations drained the
-// pipeline (cfg2 MT19937 whole run 15.8 vs 10.3 us/iter).
-hipError_t make_stream(hipStream_t* s, bool gen) {
+// The generator's stream (SPGG_GEN_STREAM_MODE): CU-masked streams are BLOCKING -- every
+// operation on the legacy null stream (torch's default: the engine's stream ordering and host
+// syncs) then waits for the generator's queued chunks.  For a small batch that serialises the
+// pipeline (MT19937 whole runs, plain non-blocking vs CU-masked: cfg2 11.1 vs 15.8 us/iter,
+// cfg4 16.8 vs 22.7, cfg5 32.3 vs 52.1); a batch that fills the GPU (>= 2400 tiles) runs faster
+// with the generator held to the host's 256-iteration turns than concurrently with every step
+// (cfg3 84.0 vs 99.9); profiles/r03/streams.txt.  Default: mode 2 for such batches, else 0.
+hipError_t make_stream(hipStream_t* s, bool gen, bool big_batch = false) {
   const char* e = getenv(gen ? "SPGG_GEN_STREAM_MODE" : "SPGG_STREAM_MODE");
-  const int mode = e ? atoi(e) : gen ? 0 : 2;
-  if (mode == 1) {
+  const int mode = e ? atoi(e) : (gen && !big_batch) ? 0 : 2;
+  if (mode == 1 || mode == 4) {  // 1: greatest priority, 4: least (non-blocking)
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, gen ? hi : lo);  // (non-blocking)
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, mode == 1 ? hi : lo);
   } else if (mode == 2 || mode == 3) {
     int dev = 0, cus = 0;
     hipError_t r = hipGetDevice(&dev);
@@ -2400,7 +2403,8 @@ int mt_lazy_init(spgg_ctx* c) {
   if (c->gen_done[0]) return SPGG_OK;
   int rc = SPGG_OK;
   if (!c->gen_stream) {
-    rc = hip_check(c, make_stream(&c->gen_stream, true), "hipStreamCreate(gen)");
+    const long long batch = c->cfg.batch_reps > 0 ? c->cfg.batch_reps : c->cfg.n_rep;
+    rc = hip_check(c, make_stream(&c->gen_stream, true, batch * c->tiles_per_rep >= 2400), "hipStreamCreate(gen)");
     if (rc) return rc;
     c->own_gen_stream = true;
   }

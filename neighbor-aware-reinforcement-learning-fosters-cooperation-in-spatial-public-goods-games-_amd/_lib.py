@@ -13,8 +13,9 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
+GEN_ERR_SPIN = 1
 STATE_REPUTATION, STATE_ACTION = 0, 1
 RNG_INJECT, RNG_MT19937, RNG_PHILOX = 0, 1, 2
 RNG_MODES = {"inject": RNG_INJECT, "mt19937": RNG_MT19937, "philox": RNG_PHILOX}
@@ -35,7 +36,8 @@ EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create
             "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
             "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range",
-            "spgg_mt_chains", "spgg_mt_jump_poly", "spgg_stream_create", "spgg_stream_destroy")
+            "spgg_mt_chains", "spgg_mt_jump_poly", "spgg_stream_create", "spgg_stream_destroy",
+            "spgg_status", "spgg_test_set_error")
 
 
 class Config(ctypes.Structure):
@@ -131,6 +133,10 @@ def load(path: str | None = None):
         lib.spgg_stream_destroy.argtypes = [vp]
         lib.spgg_set_draw_stream.restype = ctypes.c_int
         lib.spgg_set_draw_stream.argtypes = [vp, vp]
+        lib.spgg_status.restype = ctypes.c_int
+        lib.spgg_status.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+        lib.spgg_test_set_error.restype = ctypes.c_int
+        lib.spgg_test_set_error.argtypes = [vp, ctypes.c_uint32]
         lib.spgg_build_id.restype = ctypes.c_char_p
         lib.spgg_build_id.argtypes = []
         v = lib.spgg_abi_version()

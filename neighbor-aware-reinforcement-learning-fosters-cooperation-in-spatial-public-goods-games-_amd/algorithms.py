@@ -94,6 +94,11 @@ _ALIASES = {"qlearning": "qlearning", "q-learning": "qlearning", "sarsa": "sarsa
             "expected_sarsa": "expected_sarsa", "expected-sarsa": "expected_sarsa",
             "double_qlearning": "double_qlearning", "double-q-learning": "double_qlearning"}
 
+# Modules whose operator classes the device step reproduces: this module, and the reference's
+# src/model/algorithms.py under the package path its scripts import it by
+# (scripts/run_experiments.py:10-13 puts the repository root on sys.path: src.model.algorithms).
+# A class of the same name from any other module -- a user's modified copy -- is not matched.
+_OPERATOR_MODULES = (__name__, "src.model.algorithms")
 # The reference's operator classes (algorithms.py:96, 136, 181, 237) by class name.
 _BUILTIN_CLASSES = {"QLearning": "qlearning", "SARSA": "sarsa", "ExpectedSARSA": "expected_sarsa",
                     "DoubleQLearning": "double_qlearning"}
@@ -109,8 +114,8 @@ def operator_kind(algorithm) -> str:
     (spgg.py:111-118) -- or ValueError when the device step cannot run it.
 
     Accepted: this module's four operator classes, the reference's own four
-    (src/model/algorithms.py, matched by class name and module, so an instance built
-    from the reference package drops in), and subclasses of either that add state
+    (matched by class name and the fully qualified module src.model.algorithms, so an
+    instance built from the reference package drops in), and subclasses of either that add state
     but redefine none of the operator's methods.  A subclass that overrides
     select_action / update_q_table / decay_epsilon (or Double-Q's table methods), or
     an RLAlgorithm that derives from none of the four, defines arithmetic the HIP
@@ -119,7 +124,7 @@ def operator_kind(algorithm) -> str:
     cls = type(algorithm)
     base = None
     for k in cls.__mro__:
-        if k.__module__.split(".")[-1] == "algorithms" and k.__name__ in _BUILTIN_CLASSES:
+        if k.__module__ in _OPERATOR_MODULES and k.__name__ in _BUILTIN_CLASSES:
             base = k
             break
         if k.__name__ == "RLAlgorithm" or k is object:

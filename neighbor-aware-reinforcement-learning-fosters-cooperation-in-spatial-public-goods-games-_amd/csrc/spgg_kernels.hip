@@ -1602,13 +1602,12 @@ namespace {
 //
 // The raw word stream obeys x[k+624] = x[k+397] ^ twist(x[k], x[k+1]), so the 227
 // words of a block [F, F+227) depend only on words >= 227 back: block-parallel.
-// One workgroup per replica, no barrier after the prologue:
-//   waves 0..kGenNR-1, the recurrence: the 227 positions of a block in 4 slots of lanes, two
-//     per wave (gen_slot_base), x[F+j] from x[F+j-227] (the lane's previous word of the
-//     slot, a register) and x[F+j-624], x[F+j-623] (the LDS ring, 2-3 blocks old; read one
-//     block ahead).  Each wave publishes its completed blocks (gen_done) and reads another
-//     wave's words only from blocks >= 2 behind; one wave's LDS operations complete in
-//     order.  The ring holds kGenNB blocks at fixed positions (block b at 256*(b % kGenNB),
+// One workgroup per chain, no barrier after the prologue:
+//   wave 0, the recurrence: the 227 positions of a block in 4 slots of lanes
+//     (gen_slot_base), x[F+j] from x[F+j-227] (the lane's previous word of the slot, a
+//     register) and x[F+j-624], x[F+j-623] (the LDS ring, 2-3 blocks old; read one block
+//     ahead).  It publishes its completed blocks (gen_done) every kGenPub blocks; one
+//     wave's LDS operations complete in order.  The ring holds kGenNB blocks at fixed positions (block b at 256*(b % kGenNB),
 //     + a mirror of block 0 behind the last one), so with the block loop unrolled kGenNB
 //     times every LDS address is a lane constant plus an immediate offset, and no LDS
 //     operation of the recurrence sits under a branch;
@@ -1653,39 +1652,24 @@ __host__ __device__ inline int64_t draw_words_of(int n, int alg) {
   return (int64_t)((n + 63) / 64) * 2 * draw_planes(alg);
 }
 
-#ifndef SPGG_GEN_OUT
-#define SPGG_GEN_OUT 3
-#endif
-// Timing-only generator ablations (-DSPGG_GEN_ABLATE=mask; draws are WRONG): 1 = no output
-// work (the output waves only track the frontier), 2 = no recurrence arithmetic
-#ifndef SPGG_GEN_ABLATE
-#define SPGG_GEN_ABLATE 0
-#endif
-#ifndef SPGG_GEN_NR
-#define SPGG_GEN_NR 1
-#endif
-#ifndef SPGG_GEN_SETPRIO  // wave priority of the recurrence wave(s)
-#define SPGG_GEN_SETPRIO 3
-#endif
-// Blocks between two progress publications of a lone recurrence wave (each publication waits
-// for the wave's LDS writes: one exposed LDS round trip per period); two recurrence waves
-// depend on each other's previous block and publish every block.
-#ifndef SPGG_GEN_PUB
-#define SPGG_GEN_PUB 4
-#endif
-constexpr int kGenOut = SPGG_GEN_OUT;            // output waves
-constexpr int kGenNR = SPGG_GEN_NR;              // recurrence waves (1 or 2)
-static_assert(kGenNR == 1 || kGenNR == 2, "recurrence waves: 1 or 2");
-constexpr int kGenSPW = 4 / kGenNR;              // slots per recurrence wave
-constexpr int kGenPub = kGenNR > 1 ? 1 : SPGG_GEN_PUB;
+// One recurrence wave and three output waves per chain: the A/B variants of this layout
+// (2 recurrence waves, 1-3 output waves, publication periods, wave priorities, VGPR caps,
+// timing ablations) were measured in round 3 and live in profiles/r03/rejected_gen_knobs.patch.
+constexpr int kGenOut = 3;                       // output waves
+constexpr int kGenSPW = 4;                       // slots of the lone recurrence wave
+// Blocks between two progress publications of the recurrence wave (each publication waits
+// for the wave's LDS writes: one exposed LDS round trip per period).
+constexpr int kGenPub = 4;
 static_assert(16 % kGenPub == 0, "publication period divides the unrolled block loop");
-constexpr int kGenThreads = 64 * (kGenNR + kGenOut);
+constexpr int kGenThreads = 64 * (1 + kGenOut);
 constexpr int kMtBlock = 227;                    // 624 - 397: words one dependency step produces
 constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
 constexpr int kGenNB = 16;                       // ring blocks
 constexpr int kGenRing = kGenPitch * (kGenNB + 1);  // + a mirror of block 0 behind the last one
 // Bound of every wait loop between the generator's waves (~0.5 s of s_sleep): a wait that
-// long means a defect, and the kernel then ends with wrong draws instead of hanging the GPU
+// long means a defect.  The kernel then ends instead of hanging the GPU, and records
+// SPGG_GEN_ERR_SPIN in the context's error word, which spgg_flush / spgg_status report
+// (SPGG_E_STATE): the draws of such a run are not the reference's.
 constexpr uint32_t kGenSpinMax = 1u << 23;
 
 // The 227 positions of a block in 4 slots of 64 lanes: slot s holds positions
@@ -1720,8 +1704,15 @@ struct GenArgs {
   const double* eps;       // [rep][eps_slots]
   int eps_slots;
   const int* stop_iter;
+  uint32_t* err;           // the context's error word (SPGG_GEN_ERR_*), OR-ed on a failed wait
   int n, alg;
 };
+
+// A wait between the generator's waves ran out of its bound: recorded for the host (one lane,
+// a vector global atomic).
+__device__ __forceinline__ void gen_fail(const GenArgs& g) {
+  if ((threadIdx.x & 63) == 0) atomicOr(g.err, (uint32_t)SPGG_GEN_ERR_SPIN);
+}
 
 // Flags shared through LDS between the generator's waves: relaxed workgroup-scope atomics
 // on the __shared__ array itself (plain ds_read / ds_write; through a generic pointer they
@@ -1756,20 +1747,9 @@ __device__ __forceinline__ uint32_t gen_word_pos(uint32_t k) {
 // is ph.  Word indices are relative to the chain's window (the host keeps a chain below
 // 2^31 words).  skip_stopped: replicas already absorbed are left alone (their draws are
 // never read).
-// VGPR cap (SPGG_GEN_VGPR): the generator shares CUs with the step kernel, whose 5 waves per
-// SIMD hold 5 x 96 of the 512 VGPRs; a generator wave within the remaining 32 displaces none.
-#ifndef SPGG_GEN_VGPR
-#define SPGG_GEN_VGPR 0
-#endif
-#if SPGG_GEN_VGPR
-#define SPGG_GEN_ATTR __attribute__((amdgpu_num_vgpr(SPGG_GEN_VGPR)))
-#else
-#define SPGG_GEN_ATTR
-#endif
-__global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(GenArgs g, int t0, int t1,
-                                                                               int skip_stopped) {
+__global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int t0, int t1, int skip_stopped) {
   __shared__ uint32_t ring[kGenRing];
-  __shared__ uint32_t gen_done[kGenNR][64];   // blocks recurrence wave r has completed (per lane)
+  __shared__ uint32_t gen_done[64];           // blocks the recurrence wave has published (per lane)
   __shared__ uint32_t gen_need[kGenOut][64];  // output wave w reads no word below this (per lane)
   __shared__ uint32_t pos_sh;
   const int rep = blockIdx.x / g.chains, ch = blockIdx.x - rep * g.chains, tid = threadIdx.x;
@@ -1804,7 +1784,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     if (tid == 0) pos_sh = 0;
     ph = (uint32_t)(((uint64_t)g.run_pos0[rep] + (uint64_t)(t0 - 1) * W) % 624u);
   }
-  if (tid < 64 * kGenNR) gen_done[tid >> 6][tid & 63] = 0;
+  if (tid < 64) gen_done[tid] = 0;
   if (tid < 64 * kGenOut) gen_need[tid >> 6][tid & 63] = 0;
   __syncthreads();
   const uint32_t pos0 = pos_sh;
@@ -1818,15 +1798,14 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     const uint32_t target_last = key_block(E_last) + 624;
     nblk = target_last > 624 ? (target_last - 624 + kMtBlock - 1) / kMtBlock : 0;
   }
-  if (wave < kGenNR) {
-    // ---- the recurrence: wave r owns slots [r*kGenSPW, (r+1)*kGenSPW) of every block ------
-    __builtin_amdgcn_s_setprio(SPGG_GEN_SETPRIO);  // the critical path
-    const int r = wave;
+  if (wave == 0) {
+    // ---- the recurrence: every slot of every block ------------------------------------------
+    __builtin_amdgcn_s_setprio(3);  // the critical path
     uint32_t prev[kGenSPW], ca[kGenSPW], cb[kGenSPW];
     uint32_t *wp[kGenSPW], *pa[kGenSPW], *pb[kGenSPW];  // lane addresses: own word, its two operands
 #pragma unroll
     for (int i = 0; i < kGenSPW; ++i) {
-      const int j = gen_position(r * kGenSPW + i, lane);
+      const int j = gen_position(i, lane);
       wp[i] = ring + j;
       pa[i] = ring + gen_spill(j + 57);
       pb[i] = ring + gen_spill(j + 58);
@@ -1837,10 +1816,9 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     uint32_t E = pos0 + W;
     uint32_t mb = key_block(E), target = mb + 624;
     uint32_t lim = 0;   // largest F whose block may be written (output waves' reads)
-    uint32_t mind = 0;  // blocks every recurrence wave has completed (as last read)
     int t = t0;
     uint32_t key_mb = 0, key_pos = pos0;
-    uint32_t b = 0;     // blocks this wave has completed
+    uint32_t b = 0;     // blocks completed
     // key after iteration t (words [mb, mb+624) and pos), to the snapshot ring; then the next
     auto retire = [&]() {
       uint32_t* sn = g.snap + (size_t)(t % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
@@ -1857,26 +1835,15 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
       mb = key_block(E);
       target = mb + 624;
     };
-    auto poll_done = [&]() {  // min over the recurrence waves' completed blocks
-      uint32_t m = LDS_LD(gen_done[0][0]);
-      if constexpr (kGenNR > 1) m = min(m, LDS_LD(gen_done[1][0]));
-      return __builtin_amdgcn_readfirstlane(m);
-    };
     // one block: b % kGenNB == U; operands ca/cb were read one block ahead
 #define SPGG_GEN_BLOCK(U)                                                                                 \
   {                                                                                                       \
     if (b == nblk) goto rec_done;                                                                         \
-    /* the other wave's blocks <= b-2, read by the prefetch below (block b+1's operands) */               \
-    for (uint32_t spin = 0; kGenNR > 1 && mind + 1 < b && spin < kGenSpinMax; ++spin) {                   \
-      mind = poll_done();                                                                                 \
-      if (mind + 1 < b) __builtin_amdgcn_s_sleep(1);                                                      \
-    }                                                                                                     \
-    GEN_FENCE();                                                                                          \
-    if (r == 0)                                                                                           \
-      while (t <= t1 && 624u + kMtBlock * mind >= target) retire();                                       \
+    while (t <= t1 && 624u + kMtBlock * b >= target) retire();                                            \
     const uint32_t F = 624u + kMtBlock * b;                                                               \
-    for (uint32_t spin = 0; F > lim && spin < kGenSpinMax; ++spin) { /* flow control: no output wave      \
-                                                            still reads the positions written */          \
+    uint32_t spin = 0;                                                                                    \
+    for (; F > lim && spin < kGenSpinMax; ++spin) { /* flow control: no output wave still reads the     \
+                                                       positions written */                               \
       uint32_t m = 0xffffffffu;                                                                           \
       _Pragma("unroll") for (int w = 0; w < kGenOut; ++w) m = min(m, LDS_LD(gen_need[w][0]));             \
       m = __builtin_amdgcn_readfirstlane(m);                                                              \
@@ -1884,6 +1851,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
       lim = m > 0xffffffffu - (kGenNB - 1) * kMtBlock ? 0xffffffffu : m + (kGenNB - 1) * kMtBlock;        \
       if (F > lim) __builtin_amdgcn_s_sleep(2);                                                           \
     }                                                                                                     \
+    if (spin == kGenSpinMax) gen_fail(g);                                                                 \
     GEN_FENCE();                                                                                          \
     uint32_t na[kGenSPW], nb[kGenSPW];                                                                    \
     _Pragma("unroll") for (int i = 0; i < kGenSPW; ++i) {                                                 \
@@ -1892,7 +1860,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
       nb[i] = pb[i][rb];                                                                                  \
     }                                                                                                     \
     _Pragma("unroll") for (int i = 0; i < kGenSPW; ++i) {                                                 \
-      const uint32_t x = (SPGG_GEN_ABLATE & 2) ? prev[i] ^ ca[i] : mt_next(prev[i], ca[i], cb[i]);        \
+      const uint32_t x = mt_next(prev[i], ca[i], cb[i]);                                                  \
       prev[i] = x;                                                                                        \
       wp[i][U * kGenPitch] = x;                                                                           \
       if (U == 0) wp[i][kGenNB * kGenPitch] = x; /* mirror of block 0 */                                  \
@@ -1900,13 +1868,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
       cb[i] = nb[i];                                                                                      \
     }                                                                                                     \
     ++b;                                                                                                  \
-    if constexpr (kGenNR > 1) {                                                                           \
-      LDS_ST(gen_done[r][lane], b);                                                                       \
-      mind = poll_done(); /* used by the next block */                                                    \
-    } else {                                                                                              \
-      if ((U + 1) % kGenPub == 0) LDS_ST(gen_done[r][lane], b);                                           \
-      mind = b;                                                                                           \
-    }                                                                                                     \
+    if ((U + 1) % kGenPub == 0) LDS_ST(gen_done[lane], b);                                                \
   }
     static_assert(kGenNB == 16, "the block loop below is unrolled kGenNB times");
     for (;;) {
@@ -1917,12 +1879,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     }
 #undef SPGG_GEN_BLOCK
   rec_done:
-    LDS_ST(gen_done[r][lane], b);  // (a lone wave publishes every kGenPub blocks: the rest)
-    if (r != 0) return;
-    for (uint32_t spin = 0; mind < nblk && spin < kGenSpinMax; ++spin) {  // every wave's last block
-      mind = poll_done();
-      if (mind < nblk) __builtin_amdgcn_s_sleep(1);
-    }
+    LDS_ST(gen_done[lane], b);  // (published every kGenPub blocks: the rest)
     GEN_FENCE();
     while (t <= t1) retire();  // (the frontier covers every remaining target)
     if (last_chain) {
@@ -1933,7 +1890,7 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     return;
   }
   // ---- output waves: chunks ow, ow + kGenOut, ... of each iteration, plane-major --------
-  const int ow = wave - kGenNR;
+  const int ow = wave - 1;
   const uint64_t thr_half = u53_threshold(0.5);
   const int nchunk = (g.n + 63) / 64;
   uint32_t kpos = pos0;
@@ -1950,14 +1907,14 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
       const uint32_t first = base + (dbl ? 128u : 64u) * (uint32_t)c;
       const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
       LDS_ST(gen_need[ow][lane], first);
-      for (uint32_t spin = 0; seen <= last && spin < kGenSpinMax; ++spin) {  // wait for the recurrence
-        uint32_t m = LDS_LD(gen_done[0][0]);
-        if constexpr (kGenNR > 1) m = min(m, LDS_LD(gen_done[1][0]));
-        seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(m);
+      uint32_t spin = 0;
+      for (; seen <= last && spin < kGenSpinMax; ++spin) {  // wait for the recurrence
+        seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
         if (seen <= last) __builtin_amdgcn_s_sleep(1);
       }
+      if (spin == kGenSpinMax) gen_fail(g);
       GEN_FENCE();
-      if (!(SPGG_GEN_ABLATE & 1)) {
+      {
         // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
         const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
         const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
@@ -1982,6 +1939,12 @@ __global__ __launch_bounds__(kGenThreads) SPGG_GEN_ATTR void spgg_mt_gen_kernel(
     kpos += W;
   }
   LDS_ST(gen_need[ow][lane], 0xffffffffu);  // done: never blocks the recurrence
+}
+
+// spgg_test_set_error: ORs flags into a context's generator error word, on the generator's
+// stream, as a failing wait does (tests of the error path).
+__global__ void spgg_set_err_kernel(uint32_t* err, uint32_t flags) {
+  if (threadIdx.x == 0) atomicOr(err, flags);
 }
 
 // spgg_flush (MT19937): the key the reference holds after the run -- after the last
@@ -2095,6 +2058,9 @@ struct spgg_ctx {
   hipStream_t gen_stream = nullptr;  // the generator's stream (library-owned unless set)
   bool own_gen_stream = false;
   hipEvent_t gen_done[2] = {nullptr, nullptr}, step_done[2] = {nullptr, nullptr}, gen_idle = nullptr;
+  hipEvent_t caller_ready = nullptr;  // the caller's stream at a run's first generator chunk
+  uint32_t* d_err = nullptr;         // generator error word (SPGG_GEN_ERR_*, sticky per context)
+  volatile uint32_t* h_err = nullptr;  // its pinned host copy, refreshed after every chunk
   int gen_upto = 0;                  // iterations whose generation is enqueued
   std::vector<double> kappa_host;  // the replicas' kappa as last set
   bool kappa_woke = false;         // a kappa went 0 -> nonzero since the run's iteration 1
@@ -2156,15 +2122,18 @@ void choose_mt_chains(spgg_ctx* c) {
   const spgg_config& cfg = c->cfg;
   const long long W = draw_mt_words(c->n, draw_planes(cfg.algorithm));
   int chains = 1, per = 8;
+  const long long batch = cfg.batch_reps > 0 ? cfg.batch_reps : cfg.n_rep;
   if (W >= 4096) {
     const double gen_ns = W / 227.0 * 200.0;
-    const long long batch = cfg.batch_reps > 0 ? cfg.batch_reps : cfg.n_rep;
     const double step_ns = std::max(8000.0, (double)batch * c->n * 0.015);
     const double need = 4.0 * gen_ns / step_ns;
     while (chains < 256 && chains < need) chains *= 2;
     if (chains > 1)
       per = (int)std::max((1000000 + W - 1) / W, (long long)((128 + chains - 1) / chains));
-    const double rec = draw_words_of(c->n, cfg.algorithm) * 4.0 * cfg.n_rep;  // bytes per iteration
+    // bytes per iteration of the WHOLE batch: every context of one batch (replica groups of
+    // different sizes) must get the same layout, since the caller sizes the shared draw and
+    // snapshot buffers from one of them (spgg_draw_layout)
+    const double rec = draw_words_of(c->n, cfg.algorithm) * 4.0 * batch;
     while (chains > 1 && 2.0 * chains * per * rec > 512e6) {
       if (per > 1) per = std::max(1, per / 2);
       else chains /= 2;
@@ -2350,6 +2319,7 @@ GenArgs gen_args(const spgg_ctx* c, int q = -1) {
   g.eps = c->buf.eps;
   g.eps_slots = c->cfg.iterations + 2;
   g.stop_iter = c->buf.stop_iter;
+  g.err = c->d_err;
   g.n = c->n;
   g.alg = c->cfg.algorithm;
   return g;
@@ -2400,7 +2370,7 @@ hipError_t make_stream(hipStream_t* s, bool gen, bool big_batch = false) {
 // of chunk q-2 (whose ring slots it reuses) and is enqueued when chunk q-1 starts, so it
 // overlaps the steps of chunk q-1; the steps of chunk q wait for it.
 int mt_lazy_init(spgg_ctx* c) {
-  if (c->gen_done[0]) return SPGG_OK;
+  if (c->gen_done[0] && c->h_err) return SPGG_OK;
   int rc = SPGG_OK;
   if (!c->gen_stream) {
     const long long batch = c->cfg.batch_reps > 0 ? c->cfg.batch_reps : c->cfg.n_rep;
@@ -2413,6 +2383,17 @@ int mt_lazy_init(spgg_ctx* c) {
     if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->step_done[i], hipEventDisableTiming), "hipEventCreate");
   }
   if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->gen_idle, hipEventDisableTiming), "hipEventCreate");
+  if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->caller_ready, hipEventDisableTiming), "hipEventCreate");
+  if (!rc) rc = hip_check(c, hipMalloc(&c->d_err, 4), "hipMalloc(gen err)");
+  if (!rc) rc = hip_check(c, hipMemset(c->d_err, 0, 4), "hipMemset(gen err)");
+  if (!rc) {
+    void* h = nullptr;
+    rc = hip_check(c, hipHostMalloc(&h, 4, hipHostMallocDefault), "hipHostMalloc(gen err)");
+    if (!rc) {
+      c->h_err = static_cast<volatile uint32_t*>(h);
+      *c->h_err = 0;
+    }
+  }
   if (rc || c->chains == 1) return rc;
   // chained generator: start windows, chunk keys, and the jump polynomials
   const size_t R = c->cfg.n_rep, win = R * c->chains * spgg_mt::kSplits * 624;
@@ -2452,6 +2433,8 @@ void enqueue_gen_chunk(spgg_ctx* c, int q) {
   }
   launch_gen(c, t0, t1, 1, c->gen_stream, c->chains > 1 ? q : -1);
   (void)hipEventRecord(c->gen_done[q & 1], c->gen_stream);
+  // the error word after this chunk, for spgg_status (no host sync)
+  (void)hipMemcpyAsync((void*)c->h_err, c->d_err, 4, hipMemcpyDeviceToHost, c->gen_stream);
   if (c->chains > 1 && t1 < c->cfg.iterations)
     spgg_mt::launch_jump(c->d_parts[q & 1], c->d_parts[(q + 1) & 1], c->d_polys + (size_t)J * 624, R, c->chains, -1,
                          c->buf.stop_iter, c->gen_stream);
@@ -2459,6 +2442,10 @@ void enqueue_gen_chunk(spgg_ctx* c, int q) {
 }
 
 }  // namespace
+
+#ifndef SPGG_TIMING
+#define SPGG_TIMING 0
+#endif
 
 #ifndef SPGG_BUILD_ID
 #define SPGG_BUILD_ID "unversioned"
@@ -2633,9 +2620,16 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
   }
   if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
   const int K = c->gen_chunk, T = c->cfg.iterations;
-  // timing-only knobs (results are WRONG): SPGG_TIMING=1 skips the step launches (generator
-  // alone), =2 the generator launches (steps on stale draws)
-  static const int timing = getenv("SPGG_TIMING") ? atoi(getenv("SPGG_TIMING")) : 0;
+  // timing-only builds (-DSPGG_TIMING=1: the step launches skipped, the generator alone; =2: the
+  // generator launches skipped, steps on stale draws; results are WRONG); 0 in the product
+  constexpr int timing = SPGG_TIMING;
+  if (mt && n_steps > 0 && c->gen_upto == 0) {
+    // a run's first generator chunks read mt_state, eps and stop_iter and write the draw and
+    // snapshot rings, which the caller may have just written on its own stream (e.g. torch's
+    // zero fills): the generator's stream waits for it (later chunks wait for the steps)
+    (void)hipEventRecord(c->caller_ready, s);
+    (void)hipStreamWaitEvent(c->gen_stream, c->caller_ready, 0);
+  }
   for (int t = t0; t < t0 + n_steps; ++t) {
     if (mt) {
       const int q = (t - 1) / K;
@@ -2659,10 +2653,19 @@ int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {
   if (c->cfg.rng_mode == SPGG_RNG_MT19937 && c->gen_done[0]) {
     // the generator ran ahead: wait for it, then restore each replica's key to the one the
     // reference holds (after its last executed iteration) from the snapshot ring
+    (void)hipMemcpyAsync((void*)c->h_err, c->d_err, 4, hipMemcpyDeviceToHost, c->gen_stream);
     (void)hipEventRecord(c->gen_idle, c->gen_stream);
     (void)hipStreamWaitEvent(s, c->gen_idle, 0);
-    hipLaunchKernelGGL(spgg_mt_final_kernel, dim3(c->cfg.n_rep), dim3(256), 0, s, gen_args(c), t_last);
     c->gen_upto = 0;
+    // every chunk of the run has been generated once the generator's stream drains: a wait
+    // that exhausted its bound there means wrong draws, reported instead of a silent result
+    int rc = hip_check(c, hipEventSynchronize(c->gen_idle), "spgg_flush: generator");
+    if (rc) return rc;
+    if (*c->h_err)
+      return fail(c, SPGG_E_STATE, "spgg_flush: the MT19937 draw generator failed (error word " +
+                                       std::to_string(*c->h_err) + "): a wait between its waves ran out of "
+                                       "its bound, so this run's draws are not the reference's");
+    hipLaunchKernelGGL(spgg_mt_final_kernel, dim3(c->cfg.n_rep), dim3(256), 0, s, gen_args(c), t_last);
   }
   launch_step(c, t_last + 1, 1, s);
   return hip_check(c, hipGetLastError(), "spgg_flush launch");
@@ -2688,6 +2691,8 @@ int spgg_draw_range(spgg_ctx* c, int32_t t0, int32_t t1, void* stream) {
   if (t0 < 1 || t1 < t0 || t1 > c->cfg.iterations || t1 - t0 + 1 > c->gen_chunk ||
       (long long)(t1 - t0 + 2) * draw_mt_words(c->n, draw_planes(c->cfg.algorithm)) >= (1LL << 31))
     return fail(c, SPGG_E_ARG, "spgg_draw_range: 1 <= t0 <= t1 <= iterations, t1 - t0 < gen chunk, < 2^31 words");
+  const int rc = mt_lazy_init(c);  // (the error word)
+  if (rc) return rc;
   launch_gen(c, t0, t1, 0, reinterpret_cast<hipStream_t>(stream));
   return hip_check(c, hipGetLastError(), "spgg_draw launch");
 }
@@ -2700,6 +2705,22 @@ int spgg_payoff(spgg_ctx* c, int32_t t, double* out, void* stream) {
   hipLaunchKernelGGL(spgg_payoff_kernel, grid, dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                      c->buf.S[(t - 1) & 1], c->d_params, out, c->cfg.L, c->n);
   return hip_check(c, hipGetLastError(), "spgg_payoff launch");
+}
+
+int spgg_status(const spgg_ctx* c, uint32_t* flags) {
+  if (!c || !flags) return SPGG_E_ARG;
+  *flags = c->h_err ? *c->h_err : 0u;
+  return SPGG_OK;
+}
+
+int spgg_test_set_error(spgg_ctx* c, uint32_t flags) {
+  if (!c) return SPGG_E_ARG;
+  if (c->cfg.rng_mode != SPGG_RNG_MT19937) return fail(c, SPGG_E_STATE, "spgg_test_set_error: MT19937 only");
+  int rc = hip_check(c, hipSetDevice(c->cfg.device), "hipSetDevice");
+  if (!rc) rc = mt_lazy_init(c);
+  if (rc) return rc;
+  hipLaunchKernelGGL(spgg_set_err_kernel, dim3(1), dim3(64), 0, c->gen_stream, c->d_err, flags);
+  return hip_check(c, hipGetLastError(), "spgg_test_set_error launch");
 }
 
 int spgg_pub_doubles(const spgg_ctx* c, int64_t* per_rep) {
@@ -2763,7 +2784,7 @@ int spgg_set_draw_stream(spgg_ctx* c, void* stream) {
 
 int spgg_destroy(spgg_ctx* c) {
   if (!c) return SPGG_OK;
-  if (c->d_params || c->d_ring || c->gen_stream || c->gen_done[0]) {
+  if (c->d_params || c->d_ring || c->gen_stream || c->gen_done[0] || c->d_err) {
     (void)hipSetDevice(c->cfg.device);
     if (c->gen_stream) (void)hipStreamSynchronize(c->gen_stream);  // no generator writes after return
     if (c->d_params) (void)hipFree(c->d_params);
@@ -2773,6 +2794,9 @@ int spgg_destroy(spgg_ctx* c) {
       if (c->step_done[i]) (void)hipEventDestroy(c->step_done[i]);
     }
     if (c->gen_idle) (void)hipEventDestroy(c->gen_idle);
+    if (c->caller_ready) (void)hipEventDestroy(c->caller_ready);
+    if (c->d_err) (void)hipFree(c->d_err);
+    if (c->h_err) (void)hipHostFree((void*)c->h_err);
     for (int i = 0; i < 2; ++i) {
       if (c->d_parts[i]) (void)hipFree(c->d_parts[i]);
       if (c->d_keybuf[i]) (void)hipFree(c->d_keybuf[i]);

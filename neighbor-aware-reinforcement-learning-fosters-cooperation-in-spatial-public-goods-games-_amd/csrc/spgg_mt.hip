@@ -206,6 +206,9 @@ __global__ __launch_bounds__(kThreads) void mt_jump_kernel(const uint32_t* in, u
   __syncthreads();
   for (int u = tid; u < ncap; u += kThreads)
     if (1 + i0 + u < kKey) cap[u] = ring[1 + i0 + u];
+  // the copy above reads ring[1 .. 623]; the extension below overwrites those words once it
+  // wraps (m >= kRingW), so every wave's copy must be done first
+  __syncthreads();
   if (tid < 64) {  // one wave extends the stream: its LDS accesses complete in order
     const int lane = tid, mmax = i1 + kKey - 1;
     for (int F = kKey; F <= mmax; F += kBlk) {

@@ -338,10 +338,10 @@ class BatchEngine:
             C.check(self.lib.spgg_set_params(ctx, arr), ctx, "spgg_set_params")
             # border records and history-record stripes: library-defined sizes, which the
             # shared buffers' per-replica strides assume to be the same for every group
-            layout = self._layout(ctx)
+            layout = self._layout(ctx) + (self._draw_layout(ctx), self._mt_chains(ctx))
             if g == 0:
                 self.layout = layout
-                tile, per, self.stripes = layout
+                tile, per, self.stripes = layout[:3]
                 self.pub = torch.zeros((2, self.R, max(1, per)), dtype=torch.float64, device=self.dev)
                 self.stats = torch.zeros((self.R, self.stripes, self.T + 2, C.NSTAT), dtype=torch.float64,
                                          device=self.dev)
@@ -354,8 +354,9 @@ class BatchEngine:
                 self.mt_snap = torch.zeros((snaps, self.R, 625) if self.rng == "mt19937" else (1, 1, 1),
                                            dtype=torch.int32, device=self.dev)
             elif layout != self.layout:
-                raise C.SpggError(f"replica group {g} got tiling {layout} != group 0's {self.layout} "
-                                  "(tile, border-record doubles, stripes): shared buffer strides would disagree")
+                raise C.SpggError(f"replica group {g} got layout {layout} != group 0's {self.layout} "
+                                  "(tile, border-record doubles, stripes, draw ring, MT chains): shared buffer "
+                                  "strides would disagree")
             b = C.Buffers()   # the group's replica slice of every buffer
             for i in range(2):
                 b.S[i], b.R[i] = self.S[i][r0].data_ptr(), self.Rep[i][r0].data_ptr()
@@ -373,6 +374,7 @@ class BatchEngine:
         self.streams = streams
         self.ctx = self.groups[0]["ctx"]
         self.tile = self.layout[0]
+        self.mt_layout = self.layout[4]
 
     def _draw_layout(self, ctx):
         """(ring slots, u32 words per replica and slot, key-snapshot slots) of the draw records."""
@@ -380,6 +382,22 @@ class BatchEngine:
         C.check(self.lib.spgg_draw_layout(ctx, ctypes.byref(slots), ctypes.byref(words), ctypes.byref(snaps)),
                 ctx, "spgg_draw_layout")
         return int(slots.value), int(words.value), int(snaps.value)
+
+    def _mt_chains(self, ctx):
+        """(chains per replica, iterations per chain) of the MT19937 generator (1, 1 otherwise)."""
+        ch, per = ctypes.c_int32(), ctypes.c_int32()
+        C.check(self.lib.spgg_mt_chains(ctx, ctypes.byref(ch), ctypes.byref(per)), ctx, "spgg_mt_chains")
+        return int(ch.value), int(per.value)
+
+    def check_status(self):
+        """Raise if a replica group's draw generator reported an error (spgg_status: the pinned
+        copy of its error word after the last completed chunk; no sync)."""
+        for g in self.groups:
+            f = ctypes.c_uint32()
+            C.check(self.lib.spgg_status(g["ctx"], ctypes.byref(f)), g["ctx"], "spgg_status")
+            if f.value:
+                raise C.SpggError(f"replica group {self.groups.index(g)}: the MT19937 draw generator failed "
+                                  f"(error word {f.value}); the run's draws are not the reference's")
 
     def draw_record(self, t):
         """(planes, R, n) uint8 0/1 view of iteration t's draw record (unpacked on the host)."""
@@ -497,6 +515,7 @@ class BatchEngine:
         stopped is retired: its later launches would only stage loads and exit (every
         workgroup of an absorbed replica returns before computing), so they are skipped."""
         self.stopped = self.stop_iter.cpu().numpy().astype(np.int64)
+        self.check_status()
         if self.skip_dead:
             for g in self.groups:
                 if g["live"] and np.all(self.stopped[g["r0"]:g["r1"]] != 0):

@@ -95,3 +95,19 @@ def test_library_build_id_matches_sources(tmp_path):
     stale.write_bytes(data)
     assert B.needs_build(str(stale))
     assert B.library_build_id(str(stale)) == "0" * 16
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_only_documented_environment_knobs_are_read():
+    """The shipped library names no timing-only knob (SPGG_TIMING, SPGG_ABLATE, generator A/B
+    switches: compile-time defines of tuning builds whose results are wrong by design); every
+    SPGG_* string it carries is a layout / scheduling knob documented in spgg_abi.h."""
+    data = open(_lib.LIB_PATH, "rb").read()
+    names = {m.decode() for m in re.findall(rb"SPGG_[A-Z0-9_]+", data)}
+    for bad in ("SPGG_TIMING", "SPGG_ABLATE", "SPGG_STAMPS", "SPGG_GEN_ABLATE", "SPGG_GEN_NR", "SPGG_GEN_OUT",
+                "SPGG_GEN_PUB", "SPGG_GEN_SETPRIO", "SPGG_GEN_VGPR"):
+        assert bad not in names, bad
+    header = open(HEADER).read()
+    knobs = header[header.index("Environment knobs"):header.index("int spgg_create")]
+    undocumented = sorted(n for n in names if n not in knobs)
+    assert not undocumented, undocumented

@@ -16,7 +16,7 @@ from spgg_amd import algorithms as A
 def _reference_style_module():
     """A module shaped like the reference's src/model/algorithms.py (class names, ABC
     methods, hyper-parameters), standing in for an instance built from that package."""
-    mod = types.ModuleType("refsim.model.algorithms")
+    mod = types.ModuleType("src.model.algorithms")
 
     class RLAlgorithm(ABC):
         def __init__(self, alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs):
@@ -146,6 +146,28 @@ def test_reference_style_instances():
             SPGG(L=6, iterations=3, algorithm=RefCustom(**HP))
     finally:
         sys.modules.pop(ref.__name__, None)
+
+
+def test_same_named_class_from_another_module_is_refused():
+    """A user's modified copy of the reference's algorithms.py (my/algorithms.py) defines a
+    class named QLearning whose update differs: only the reference's own module path
+    (src.model.algorithms) and this package's are matched, so the copy is refused instead of
+    silently running the built-in operator's arithmetic."""
+    mod = types.ModuleType("my.algorithms")
+
+    class RLAlgorithm(ABC):
+        def __init__(self, alpha, gamma, epsilon, epsilon_decay, epsilon_min, **kwargs):
+            self.alpha, self.gamma, self.epsilon = alpha, gamma, epsilon
+            self.epsilon_decay, self.epsilon_min = epsilon_decay, epsilon_min
+
+    class QLearning(RLAlgorithm):
+        def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
+            return q_table * 0.5   # the modification
+
+    for cls in (RLAlgorithm, QLearning):
+        cls.__module__ = mod.__name__
+    with pytest.raises(ValueError, match=r"my\.algorithms\..*QLearning.*update_q_table"):
+        SPGG(L=6, iterations=3, algorithm=QLearning(**HP))
 
 
 def test_non_operator_is_refused_like_the_reference():

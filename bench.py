@@ -65,26 +65,67 @@ def workload(name, rank):
     raise SystemExit(f"unknown config {name}")
 
 
-def cpu_baseline(L, M2, state, reps, budget_s=15.0):
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), or the platform's processor string."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def available_cpus():
+    """CPUs this process may run on: its affinity mask, capped by a cgroup CPU quota
+    (cgroup v2 cpu.max) -- on a GPU box os.cpu_count() shows the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    # the job's CPU share as the scheduler states it (the GPU pool sets OMP_NUM_THREADS to it)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
+def cpu_baseline(L, M2, state, reps, budget_s=15.0, budget_1proc_s=8.0):
     """Oracle (NumPy restatement of the reference step, same diagnostics) on host cores.
 
-    Bounded sample of the same workload: up to 16 replicas, each stepped by its
-    own process (the reference's own Pool parallelism, runner.py:142) for
-    budget_s of wall time after a short warm-up; the rate counts the agent-steps
-    those processes completed inside their timed windows."""
+    Bounded samples of the same workload (CPU timing plan 2):
+      * 1 process stepping the workload's first replica for budget_1proc_s (value_1proc:
+        the per-replica rate of the reference's own serial SPGG.run);
+      * the reference's Pool parallelism (runner.py:142): min(available CPUs, replicas)
+        processes, each stepping one replica of the workload for budget_s.
+    The rates count the agent-steps completed inside the timed windows (after 3 warm-up
+    iterations)."""
     import multiprocessing as mp
-    procs = max(1, min(16, os.cpu_count() or 1, len(reps)))
+    avail = available_cpus()
+    procs = max(1, min(avail, len(reps)))
+    ctx = mp.get_context("spawn")   # spawned workers: the parent holds a HIP context; workers are NumPy only
+    with ctx.Pool(1) as pool:
+        one = pool.map(_cpu_job, [(L, M2, state, reps[0], budget_1proc_s)])[0]
     jobs = [(L, M2, state, reps[i % len(reps)], budget_s) for i in range(procs)]
-    # spawned (not forked) workers: the parent holds a HIP context; the workers are NumPy only
-    with mp.get_context("spawn").Pool(procs) as pool:
+    with ctx.Pool(procs) as pool:
         done = pool.map(_cpu_job, jobs)
     steps = sum(d[0] for d in done)
     wall = max(d[1] for d in done)
     agent_steps = steps * L * L
     out = {"value": agent_steps / wall, "unit": "agent-steps/s", "cores": procs, "kind": "port",
-           "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics), {procs} processes, each stepping "
-                     f"one L={L} replica of the same workload for {budget_s:.0f} s after 3 warm-up "
-                     f"iterations; {steps} iterations in {wall:.1f} s wall"}
+           "value_1proc": one[0] * L * L / one[1], "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+           "available_cpus": avail,
+           "sample": f"oracle/spgg_oracle.py (NumPy, with diagnostics): {procs} processes (min of the "
+                     f"{avail} CPUs available to this process and the workload's {len(reps)} replicas), each "
+                     f"stepping one L={L} replica of the same workload for {budget_s:.0f} s after 3 warm-up "
+                     f"iterations, {steps} iterations in {wall:.1f} s wall; value_1proc: one process alone, "
+                     f"{one[0]} iterations in {one[1]:.1f} s"}
     # the oracle's speed relative to the reference's own SPGG.run on the same core
     # (tools/calibrate_cpu.py, survey container; the reference never travels)
     cal = os.path.join(ROOT, "profiles", "r03", "cpu_calibration.json")
@@ -92,7 +133,9 @@ def cpu_baseline(L, M2, state, reps, budget_s=15.0):
         c = json.load(open(cal))
         out["oracle_over_reference"] = c["oracle_over_reference"]
         out["reference_equivalent_value"] = out["value"] / c["oracle_over_reference"]
-        out["calibration"] = (f"profiles/r03/cpu_calibration.json: {c['workload']}; reference "
+        out["reference_equivalent_value_1proc"] = out["value_1proc"] / c["oracle_over_reference"]
+        out["calibration"] = (f"profiles/r03/cpu_calibration.json (measured in the survey container, where "
+                              f"the reference can run; not this host): {c['workload']}; reference "
                               f"{c['reference_ms_per_iteration']:.1f} ms/iteration vs oracle "
                               f"{c['oracle_ms_per_iteration']:.1f}, one core of {c['cpu']}")
     return out
@@ -160,7 +203,7 @@ def full_run(L, M2, state, reps, rng, streams, T, offset):
             "note": "whole run through BatchEngine.run (absorbing stops, group retirement, host syncs, flush)"}
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -181,22 +224,29 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-mt", action="store_true",
                     help="skip the MT19937 (product-path) window reported beside a Philox line")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
     import numpy as np
     import torch
     import spgg_amd
-    from spgg_amd.engine import BatchEngine
+    from spgg_amd import engine as E
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist = None
+    # the collectives' backend: RCCL ("nccl") on the GPUs; $SPGG_DIST_BACKEND=gloo for the CPU test
+    # of this launch path (tests/test_bench_world_cpu.py), whose collectives then run on host tensors
+    backend = os.environ.get("SPGG_DIST_BACKEND", "nccl")
+    coll_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     desc, L, M2, state, reps = workload(args.config, rank)
     if args.replicas:
@@ -209,14 +259,11 @@ def main():
     def window(rng):
         """W untimed + K timed iterations of a fresh engine in `rng` mode (barrier +
         synchronize on both sides; max over ranks): the executed agent-steps, times, layout."""
-        eng = BatchEngine(L, K + W, reps, use_second_order=M2, state_representation=state, rng=rng,
-                          streams=args.streams, replica_offset=rank * len(reps))
+        eng = E.BatchEngine(L, K + W, reps, use_second_order=M2, state_representation=state, rng=rng,
+                            streams=args.streams, replica_offset=rank * len(reps))
         mt_layout = None
         if rng == "mt19937":  # the draw generator's chains (spgg_mt_chains)
-            import ctypes
-            ch, per = ctypes.c_int32(), ctypes.c_int32()
-            eng.lib.spgg_mt_chains(eng.ctx, ctypes.byref(ch), ctypes.byref(per))
-            mt_layout = {"chains_per_replica": ch.value, "iterations_per_chain": per.value}
+            mt_layout = {"chains_per_replica": eng.mt_layout[0], "iterations_per_chain": eng.mt_layout[1]}
         eng.step(W)
         torch.cuda.synchronize()
         if dist:
@@ -240,7 +287,10 @@ def main():
         agent_steps = float(executed.sum()) * L * L
         ncoop = eng.stats_folded()[:, :, 0].cpu().numpy()  # SPGG_ST_NCOOP per iteration slot
         coop = np.array([ncoop[k, int(last[k]) + 1] / (L * L) for k in range(len(reps))])
-        tot = torch.tensor([agent_steps, wall], dtype=torch.float64, device=torch.device("cuda", local))
+        # the window's cooperation-rate trace (iterations W+1 .. W+K; NaN after an absorbing stop)
+        trace = ncoop[:, W + 1:W + K + 1] / (L * L)
+        trace[np.arange(K)[None, :] + W + 1 > last[:, None] + 1] = np.nan
+        tot = torch.tensor([agent_steps, wall], dtype=torch.float64, device=coll_dev)
         if dist:
             s_ = tot[:1].clone()
             dist.all_reduce(s_, op=dist.ReduceOp.SUM)
@@ -250,8 +300,8 @@ def main():
         else:
             agent_steps_all, wall_max = agent_steps, wall
         out = dict(agent_steps=agent_steps, agent_steps_all=agent_steps_all, wall=wall, wall_max=wall_max,
-                   dev_ms=dev_ms, coop=coop, mt_layout=mt_layout, resident=eng.resident, groups=eng.G,
-                   waves=eng.waves)
+                   dev_ms=dev_ms, coop=coop, trace=trace, mt_layout=mt_layout, resident=eng.resident,
+                   groups=eng.G, waves=eng.waves)
         eng.close()   # before the next engine, the full run and the CPU baseline's worker processes
         return out
 
@@ -259,11 +309,15 @@ def main():
     main_w = window(args.rng)
     agent_steps, wall, dev_ms = main_w["agent_steps"], main_w["wall"], main_w["dev_ms"]
     agent_steps_all, wall_max, mt_layout = main_w["agent_steps_all"], main_w["wall_max"], main_w["mt_layout"]
-    # final cooperation-rate gather over RCCL (the path's only collective)
-    coop = torch.from_numpy(main_w["coop"]).to(torch.device("cuda", local))
+    # the path's only collective: every rank's per-replica final
+    # cooperation rate and cooperation-rate trace, all-gathered (RCCL over xGMI on the GPUs)
+    rows = np.concatenate([main_w["coop"][:, None], main_w["trace"]], axis=1)
+    gathered_rows = rows[None]
     if dist:
-        gathered = [torch.empty_like(coop) for _ in range(world)]
-        dist.all_gather(gathered, coop)
+        buf = torch.from_numpy(np.ascontiguousarray(rows)).to(coll_dev)
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        gathered_rows = np.stack([p_.cpu().numpy() for p_ in parts])
     value = agent_steps_all / wall_max
     per_step_dev_s = dev_ms / 1e3 / K
     step_agents = agent_steps / K
@@ -289,6 +343,11 @@ def main():
                        "rng": args.rng, "streams_per_gpu": resident, "replica_groups": groups,
                        "cache_waves": waves, "mt_chains": mt_layout,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
+            "gather": {"replicas": int(gathered_rows.shape[0] * gathered_rows.shape[1]),
+                       "bytes": int(gathered_rows.nbytes),
+                       "mean_final_coop": float(np.mean(gathered_rows[:, :, 0])),
+                       "what": "per-replica final cooperation rate + the window's cooperation-rate trace, "
+                               "all_gather over every rank"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "time_base": "HIP events around the K timed iterations (device time per iteration)",

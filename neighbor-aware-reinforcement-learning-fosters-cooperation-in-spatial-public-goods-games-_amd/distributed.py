@@ -95,17 +95,37 @@ def gather_rows(local: np.ndarray, n_items: int, device=None, group=None) -> np.
     return out
 
 
-SUMMARY_FIELDS = ("final_coop", "final_def", "stop_iter", "iterations_run")
+# per replica the final cooperation / defection rates and mean P (the
+# return value of the reference's SPGG.run, spgg.py:635-637), the absorbing iteration and the
+# iterations run; plus, separately, the cooperation-rate trace (coop_traces)
+SUMMARY_FIELDS = ("final_coop", "final_def", "mean_P", "stop_iter", "iterations_run")
 
 
 def replica_summaries(engine) -> np.ndarray:
-    """(R, 4) float64 per-replica summary of a finished BatchEngine."""
-    out = np.zeros((engine.R, len(SUMMARY_FIELDS)))
-    for k in range(engine.R):
+    """(R, 5) float64 per-replica summary of a finished BatchEngine.  mean_P is the mean payoff
+    of the last iteration a replica started (spgg.py:378, 637): P from S_last, which sits in
+    ping-pong buffer (last - 1) & 1 (an absorbed replica's buffers are frozen), so at most two
+    payoff launches cover the batch."""
+    R = engine.R
+    out = np.zeros((R, len(SUMMARY_FIELDS)))
+    lasts = [int(engine.last_iteration(k)) for k in range(R)]
+    P = {par: engine.payoff_at(par + 1) for par in sorted({(t - 1) & 1 for t in lasts if t >= 1})}
+    for k in range(R):
         _, _, S = engine.final_state(k)
         n = S.size
         c = float(np.sum(S == 0)) / n
-        out[k] = (c, 1.0 - c, float(engine.stopped[k]), float(engine.last_iteration(k)))
+        mp = float(np.mean(P[(lasts[k] - 1) & 1][k])) if lasts[k] >= 1 else float("nan")
+        out[k] = (c, 1.0 - c, mp, float(engine.stopped[k]), float(lasts[k]))
+    return out
+
+
+def coop_traces(engine) -> np.ndarray:
+    """(R, iterations) float64 cooperation rate at the start of every iteration (the reference's
+    coop_rate_history, spgg.py:383, 595), NaN after a replica's last iteration."""
+    st = engine.stats_folded()[:, 1:engine.T + 1, 0].cpu().numpy()   # SPGG_ST_NCOOP, slots 1..T
+    out = st / float(engine.L * engine.L)
+    lasts = np.array([engine.last_iteration(k) for k in range(engine.R)])
+    out[np.arange(engine.T)[None, :] + 1 > lasts[:, None]] = np.nan
     return out
 
 
@@ -116,7 +136,8 @@ def run_sharded(replicas, L: int, iterations: int, use_second_order=True,
     The rank's GPU is LOCAL_RANK (torchrun) unless `device` names one; replica k of
     the block keeps its global index (shard offset + k) as its Philox stream id, so a
     replica's stream -- and its trajectory in "philox" mode -- does not depend on the
-    world size.  Returns (summaries (N, 4) on every rank, this rank's BatchEngine)."""
+    world size.  Returns (summaries (N, 5) and cooperation-rate traces (N, iterations), both
+    on every rank, and this rank's BatchEngine) -- the one collective of the path."""
     import torch.distributed as dist
     from . import engine as E
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -129,13 +150,16 @@ def run_sharded(replicas, L: int, iterations: int, use_second_order=True,
     mine = list(replicas[a:b])
     eng = None
     local = np.zeros((0, len(SUMMARY_FIELDS)))
+    traces = np.zeros((0, iterations))
     if mine:
         eng = E.BatchEngine(L, iterations, mine, use_second_order=use_second_order,
                             state_representation=state_representation, rng=rng, device=device,
                             replica_offset=a)
         eng.run(snapshots=False)
         local = replica_summaries(eng)
+        traces = coop_traces(eng)
     if world == 1:
-        return local, eng
+        return local, traces, eng
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else None
-    return gather_rows(local, len(replicas), device=dev, group=group), eng
+    rows = gather_rows(np.concatenate([local, traces], axis=1), len(replicas), device=dev, group=group)
+    return rows[:, :len(SUMMARY_FIELDS)], rows[:, len(SUMMARY_FIELDS):], eng

@@ -47,6 +47,15 @@ class _FakeEngine:
     def last_iteration(self, k):
         return self.T
 
+    def payoff_at(self, t):                          # P = seed / 100 everywhere, from S_t's buffer
+        return np.stack([np.full((self.L, self.L), p.seed / 100.0) for p in self.reps])
+
+    def stats_folded(self):                          # NCOOP of slot t = seed + t
+        st = torch.zeros((self.R, self.T + 2, 34), dtype=torch.float64)
+        for k, p in enumerate(self.reps):
+            st[k, :, 0] = torch.arange(self.T + 2, dtype=torch.float64) + p.seed
+        return st
+
 
 def _worker(rank, world, ports, q):
     import spgg_amd  # noqa: F401
@@ -81,8 +90,9 @@ def _worker(rank, world, ports, q):
         out["rx_results"] = [(p, c) for p, (c, _) in res]
         out["rx_ran"] = ran[:]
         reps = [ReplicaParams(r=3.0, seed=s) for s in range(5, 12)]    # 7 replicas
-        summ, eng = D.run_sharded(reps, L=4, iterations=9, rng="philox")
+        summ, traces, eng = D.run_sharded(reps, L=4, iterations=9, rng="philox")
         out["sharded"] = summ
+        out["traces"] = traces
         out["engine"] = _FakeEngine.made[-1]
     finally:
         dist.destroy_process_group()
@@ -132,8 +142,10 @@ def test_launch_path_world2_gloo():
         e = o["engine"]
         assert e["seeds"] == list(range(5 + a, 5 + b)) and e["offset"] == a
         assert e["device"] == o["rank"] and e["cur_dev"] == o["rank"]
-        want = np.array([[s / 16, 1 - s / 16, 0.0, 9.0] for s in range(5, 12)])
+        want = np.array([[s / 16, 1 - s / 16, s / 100, 0.0, 9.0] for s in range(5, 12)])
         np.testing.assert_allclose(o["sharded"], want)
+        # the cooperation-rate traces of every replica, gathered in replica order
+        np.testing.assert_allclose(o["traces"], [[(s + t) / 16 for t in range(1, 10)] for s in range(5, 12)])
 
     # sweep.main under torchrun env: each rank runs its block only, results complete
     cfg = SW.load_config(None)

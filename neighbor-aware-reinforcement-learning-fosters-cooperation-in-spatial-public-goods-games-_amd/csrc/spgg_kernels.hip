@@ -1517,6 +1517,17 @@ void launch_t(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_
                        fin);
     return;
   }
+  if constexpr (APT > 2) {
+    if (lc.apt == 2) {  // two agents per thread (tiles of <= 512 agents: 20 x 25 when 20 divides L)
+      if (lc.twc == 20)
+        hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 2, 20, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
+                           t, fin);
+      else
+        hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, 2, 0, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
+                           t, fin);
+      return;
+    }
+  }
 #ifndef SPGG_NO_TWC
   if (lc.twc == 40)  // the tile every L that is a multiple of 40 gets (L = 200, 1000)
     hipLaunchKernelGGL((spgg_step_kernel<M2, AS, RQ, RNG, APT, 40, ALG>), grid, dim3(kBlock), lc.lds_bytes, s, a,
@@ -2080,7 +2091,10 @@ namespace {
 // full width, L >= 2 * window width (L % 4 == 0 for the aligned-dword window
 // staging), window rows within the staging register budget (TH <= 25).
 int twc_of(const spgg_config& cfg, int TW, int TH) {
-  return (TW == 40 && cfg.L % 40 == 0 && cfg.L >= 120 && TH <= 25) ? 40 : 0;
+  if (TW == 40 && cfg.L % 40 == 0 && cfg.L >= 120 && TH <= 25) return 40;
+  // two agents per thread (spgg_create): 20 x 25 tiles, kernels of compile-time width 20
+  if (TW == 20 && cfg.L % 20 == 0 && cfg.L >= 60 && TH <= 25 && cfg.algorithm != SPGG_ALG_DOUBLE_Q) return 20;
+  return 0;
 }
 
 // spgg_last_error(NULL): the calling thread's last spgg_create failure
@@ -2502,8 +2516,9 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     if (const char* e = getenv("SPGG_APT")) {
       if (!strcmp(e, "max") || atoi(e) == apt_max) apt = apt_max;
       else if (!strcmp(e, "1")) apt = 1;
+      else if (!strcmp(e, "2")) apt = 2;
       else
-        return create_fail(SPGG_E_ARG, std::string("SPGG_APT=") + e + ": expected 1 or max (" +
+        return create_fail(SPGG_E_ARG, std::string("SPGG_APT=") + e + ": expected 1, 2 or max (" +
                                            std::to_string(apt_max) + " agents per thread for this operator)");
     } else if (tiles4 < kSmallBatchTiles) {
       apt = 1;
@@ -2519,6 +2534,12 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->snap_slots = 3 * c->gen_chunk + 1;
   c->draw_words = draw_words_of(c->n, cfg->algorithm);
   choose_tile(cfg->L, kBlock * c->apt, &c->TW, &c->TH);
+  // two agents per thread: 20 x 25 (500 agents) where 20 divides L -- the same cost as the
+  // chooser's 25 x 20 (a transpose), with a compile-time tile width (aligned-dword windows)
+  if (c->apt == 2 && c->apt < spgg_impl::apt_of(cfg->algorithm) && cfg->L % 20 == 0 && cfg->L >= 60) {
+    c->TW = 20;
+    c->TH = 25;
+  }
   if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;
     if (sscanf(e, "%dx%d", &w, &h) == 2 && w >= 1 && h >= 1 && w <= std::min(cfg->L, 56) &&

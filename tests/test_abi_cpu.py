@@ -71,10 +71,10 @@ def test_create_failures_report_a_reason(monkeypatch):
     monkeypatch.setenv("SPGG_APT", "3")
     rc, msg = create()
     assert rc == _lib.E_ARG and "SPGG_APT=3" in msg and "max" in msg
-    monkeypatch.setenv("SPGG_APT", "2")   # Double-Q's maximum, not Q-learning's
-    rc, msg = create(algorithm=_lib.ALG_QLEARNING)
-    assert rc == _lib.E_ARG and "4 agents per thread" in msg
-    with pytest.raises(_lib.SpggError, match="SPGG_APT=2"):
+    monkeypatch.setenv("SPGG_APT", "4")   # Q-learning's maximum, not Double-Q's
+    rc, msg = create(algorithm=_lib.ALG_DOUBLE_Q)
+    assert rc == _lib.E_ARG and "2 agents per thread" in msg
+    with pytest.raises(_lib.SpggError, match="SPGG_APT=4"):
         _lib.check(rc, None, "spgg_create")
 
 

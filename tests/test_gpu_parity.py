@@ -96,7 +96,8 @@ def _oracle_final(L, T, p, seed, M2, state, algorithm="qlearning"):
 
 
 def _force_apt(monkeypatch, apt, alg="qlearning"):
-    """Agents per thread of the step kernel: "1" (small-batch mode) or "max" (4; Double-Q 2)."""
+    """Agents per thread of the step kernel: "1" (small-batch mode), "2" (20 x 25 tiles where 20
+    divides L) or "max" (4; Double-Q 2)."""
     monkeypatch.setenv("SPGG_APT", apt)
 
 
@@ -108,7 +109,7 @@ def _runner_params(**kw):
     return ReplicaParams(**base)
 
 
-@pytest.mark.parametrize("apt", ["1", "max"])
+@pytest.mark.parametrize("apt", ["1", "2", "max"])
 @pytest.mark.parametrize("M2,state", [(False, "reputation"), (True, "action"), (True, "reputation")])
 def test_batched_replicas_match_oracle(M2, state, apt, monkeypatch):
     _force_apt(monkeypatch, apt)
@@ -282,12 +283,14 @@ def test_mt_chained_generator_vs_oracle(chains, per, alg, monkeypatch):
         eng.close()
 
 
-@pytest.mark.parametrize("apt", ["1", "max"])
+@pytest.mark.parametrize("apt", ["1", "2", "max"])
 @pytest.mark.parametrize("L,T,M2", [(200, 150, False), (200, 60, True), (1000, 3, False)])
 def test_full_size_bit_exact(L, T, M2, apt, monkeypatch):
     _force_apt(monkeypatch, apt)
     p = _runner_params(seed=0)
     eng = BatchEngine(L, T, [p], use_second_order=M2, rng="mt19937")
+    if apt == "2":
+        assert eng.tile == (20, 25)   # the compile-time width 20 instance
     eng.run(snapshots=False)
     ds, fin = _oracle_final(L, T, p, 0, M2, "reputation")
     Q, R, S = eng.final_state(0)
@@ -455,16 +458,18 @@ def test_cache_blocked_waves_match_concurrent_groups(rng, monkeypatch):
     (False, "reputation", "double_qlearning", 0.3),
     (True, "reputation", "qlearning", 1.0),
 ])
-def test_compile_time_width_paths_bit_exact(M2, state, alg, gain, monkeypatch):
+@pytest.mark.parametrize("apt", ["2", "max"])
+def test_compile_time_width_paths_bit_exact(M2, state, alg, gain, apt, monkeypatch):
     """Kernels of compile-time tile width (L % 40 == 0: aligned-dword window staging, one LDS
-    pitch) for every operator, order, state representation and reputation storage."""
-    _force_apt(monkeypatch, "max", alg)
+    pitch; two agents per thread: width 20) for every operator, order, state representation
+    and reputation storage."""
+    _force_apt(monkeypatch, apt, alg)
     L, T = 120, 40
     reps = [_runner_params(seed=s, rep_gain_C=gain, r=3.0 + 0.4 * s) for s in (5, 6)]
     eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng="mt19937",
                       algorithm=alg)
     if alg != "double_qlearning":   # Double-Q tiles hold <= 512 agents: run-time width
-        assert eng.tile == (40, 24)
+        assert eng.tile == ((40, 24) if apt == "max" else (20, 25))
     eng.run(snapshots=False)
     for k, p in enumerate(reps):
         ds, fin = _oracle_final(L, T, p, p.seed, M2, state, algorithm=alg)
@@ -595,19 +600,20 @@ def test_philox_results_independent_of_tiling(M2, state, monkeypatch):
     L, T = 200, 40
     reps = [_runner_params(r=3.0 + 0.5 * s, influence_factor=1.0, seed=80 + s) for s in range(3)]
     res = {}
-    for apt in ("1", "max"):
+    for apt in ("1", "2", "max"):
         _force_apt(monkeypatch, apt)
         eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng="philox")
         eng.run(snapshots=False)
         res[apt] = (eng.tile, [eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy())
         eng.close()
-    assert res["1"][0] != res["max"][0]
-    for a, b in zip(res["1"][1], res["max"][1]):
-        for x, y in zip(a, b):
-            assert np.array_equal(x, y)
-    # history records: the same values summed over different tile partitions (f32 NI-percent
-    # partials per workgroup): equal to rounding, far inside the 1e-5 history tolerance
-    np.testing.assert_allclose(res["1"][2], res["max"][2], rtol=1e-6, atol=1e-9)
+    assert len({res[a][0] for a in res}) == 3
+    for other in ("2", "max"):
+        for a, b in zip(res["1"][1], res[other][1]):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y)
+        # history records: the same values summed over different tile partitions (f32 NI-percent
+        # partials per workgroup): equal to rounding, far inside the 1e-5 history tolerance
+        np.testing.assert_allclose(res["1"][2], res[other][2], rtol=1e-6, atol=1e-9)
 
 
 @pytest.mark.gpu

@@ -1672,6 +1672,9 @@ constexpr int kGenSPW = 4;                       // slots of the lone recurrence
 // for the wave's LDS writes: one exposed LDS round trip per period).
 constexpr int kGenPub = 4;
 static_assert(16 % kGenPub == 0, "publication period divides the unrolled block loop");
+// Chunks between two publications of an output wave's need (the recurrence may run 15 blocks,
+// 3405 words, past the smallest need; a wave's need lags its reads by < 2 x 3 x 128 words).
+constexpr int kGenNeedEvery = 2;
 constexpr int kGenThreads = 64 * (1 + kGenOut);
 constexpr int kMtBlock = 227;                    // 624 - 397: words one dependency step produces
 constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
@@ -1900,52 +1903,57 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     }
     return;
   }
-  // ---- output waves: chunks ow, ow + kGenOut, ... of each iteration, plane-major --------
+  // ---- output waves: chunks ow, ow + kGenOut, ... of every plane of every iteration --------
+  // (per chunk: one ring read per lane, the temper / parity, one ballot, one two-lane store;
+  // the chunk's first word is published as the wave's need every kGenNeedEvery chunks)
   const int ow = wave - 1;
   const uint64_t thr_half = u53_threshold(0.5);
   const int nchunk = (g.n + 63) / 64;
   uint32_t kpos = pos0;
   uint32_t seen = 624;  // the frontier as last read
+  uint32_t k = 0;       // chunks this wave has handled
+  const uint32_t lane_planes = (uint32_t)(lane * planes);
   for (int t = t0; t <= t1; ++t) {
     const uint64_t thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t]);
     uint32_t* rec_out = g.draws + (size_t)((t - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
-    int p = 0, c = ow;
-    while (p < planes && c >= nchunk) { c -= nchunk; ++p; }
-    while (p < planes) {
-      const uint32_t base = kpos + plane_word0((uint32_t)g.n, p);
-      const int cnt = min(64, g.n - 64 * c);
+    for (int p = 0; p < planes; ++p) {
       const bool dbl = (p & 1) == 0;
-      const uint32_t first = base + (dbl ? 128u : 64u) * (uint32_t)c;
-      const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
-      LDS_ST(gen_need[ow][lane], first);
-      uint32_t spin = 0;
-      for (; seen <= last && spin < kGenSpinMax; ++spin) {  // wait for the recurrence
-        seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
-        if (seen <= last) __builtin_amdgcn_s_sleep(1);
-      }
-      if (spin == kGenSpinMax) gen_fail(g);
-      GEN_FENCE();
-      {
+      // rand() < th: ((a>>5) * 2^26 + (b>>6)) / 2^53 < th as a 53-bit integer compare, decided
+      // by a alone unless its 27 bits equal th's (p = 2^-27: b is read only then)
+      const uint64_t th = (g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr;
+      const uint32_t th_hi = __builtin_amdgcn_readfirstlane((uint32_t)(th >> 26));
+      const uint32_t th_lo = __builtin_amdgcn_readfirstlane((uint32_t)th & ((1u << 26) - 1u));
+      const uint32_t base = kpos + plane_word0((uint32_t)g.n, p);
+      const uint32_t wstep = dbl ? 128u : 64u, wlane = dbl ? 2u * lane : (uint32_t)lane;
+      for (int c = ow; c < nchunk; c += kGenOut, ++k) {
+        const int cnt = min(64, g.n - 64 * c);
+        const uint32_t first = base + wstep * (uint32_t)c;
+        const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
+        if (k % kGenNeedEvery == 0) LDS_ST(gen_need[ow][lane], first);
+        uint32_t spin = 0;
+        for (; seen <= last && spin < kGenSpinMax; ++spin) {  // wait for the recurrence
+          seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
+          if (seen <= last) __builtin_amdgcn_s_sleep(1);
+        }
+        if (spin == kGenSpinMax) gen_fail(g);
+        GEN_FENCE();
         // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
         const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
         const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
+        const uint32_t o = o0 + wlane;
+        const uint32_t x = rb[gen_spill(o)];
         bool flag;
-        if (dbl) {  // rand() < thr: ((a>>5) * 2^26 + (b>>6)) / 2^53 < thr as a 53-bit integer compare,
-                    // decided by a alone unless its 27 bits equal thr's (p = 2^-27: b read only then)
-          const uint64_t th = (g.alg == SPGG_ALG_DOUBLE_Q && p == 2) ? thr_half : thr;
-          const uint32_t th_hi = (uint32_t)(th >> 26), th_lo = (uint32_t)th & ((1u << 26) - 1u);
-          const uint32_t o = o0 + 2 * lane;
-          const uint32_t ah = mt_temper(rb[gen_spill(o)]) >> 5;
+        if (dbl) {
+          const uint32_t ah = mt_temper(x) >> 5;
           flag = ah < th_hi;
           if (ah == th_hi) flag = (mt_temper(rb[gen_spill(o + 1)]) >> 6) < th_lo;
-        } else {    // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
-          flag = (__builtin_popcount(rb[gen_spill(o0 + lane)] & kTemperBit0) & 1) != 0;
+        } else {  // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
+          flag = (__builtin_popcount(x & kTemperBit0) & 1) != 0;
         }
-        const uint64_t bits = __ballot(flag && lane < cnt);  // (lanes past n read stale words)
-        if (lane < 2) rec_out[(2 * c + lane) * planes + p] = (uint32_t)(lane ? bits >> 32 : bits);
+        // (lanes past n read stale words: masked)
+        const uint64_t bits = __builtin_amdgcn_ballot_w64(flag) & (cnt == 64 ? ~0ull : (1ull << cnt) - 1ull);
+        if (lane < 2) *at(rec_out, (uint32_t)(2 * c * planes + p) + lane_planes) = (uint32_t)(lane ? bits >> 32 : bits);
       }
-      c += kGenOut;
-      while (p < planes && c >= nchunk) { c -= nchunk; ++p; }
     }
     kpos += W;
   }

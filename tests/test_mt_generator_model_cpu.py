@@ -54,7 +54,7 @@ def plane_word0(n, p):
     return n * (p // 2 * 3 + (p & 1) * 2)
 
 
-def run_model(n, planes, t0, t1, key, pos0, seed, NR, NOUT=7, PUB=4):
+def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4, NEED_EVERY=2):
     rnd = random.Random(seed)
     SPW = 4 // NR
     ring = [0] * RING
@@ -132,34 +132,29 @@ def run_model(n, planes, t0, t1, key, pos0, seed, NR, NOUT=7, PUB=4):
 
     def outw(ow):
         nchunk = (n + 63) // 64
-        kpos, seen = pos0, 624
+        kpos, seen, k = pos0, 624, 0
         for t in range(t0, t1 + 1):
-            p, c = 0, ow
-            while p < planes and c >= nchunk:
-                c -= nchunk
-                p += 1
-            while p < planes:
-                cnt, dbl = min(64, n - 64 * c), (p & 1) == 0
-                first = kpos + plane_word0(n, p) + (128 if dbl else 64) * c
-                last = first + (2 if dbl else 1) * cnt - 1
-                gen_need[ow] = first
-                yield
-                while seen <= last:
-                    seen = 624 + MB * min(gen_done)
+            for p in range(planes):
+                for c in range(ow, nchunk, NOUT):
+                    cnt, dbl = min(64, n - 64 * c), (p & 1) == 0
+                    first = kpos + plane_word0(n, p) + (128 if dbl else 64) * c
+                    last = first + (2 if dbl else 1) * cnt - 1
+                    if k % NEED_EVERY == 0:       # the need is published every NEED_EVERY chunks
+                        gen_need[ow] = first
+                        yield
+                    k += 1
+                    while seen <= last:
+                        seen = 624 + MB * min(gen_done)
+                        yield
+                    kk = first + 57
+                    B = kk // MB
+                    o0, rbase = kk - B * MB, P * ((B + NB - 3) % NB)
+                    if dbl:
+                        out[t, p, c] = [(temper(ring[rbase + spill(o0 + 2 * l)]),
+                                         temper(ring[rbase + spill(o0 + 2 * l + 1)])) for l in range(cnt)]
+                    else:
+                        out[t, p, c] = [temper(ring[rbase + spill(o0 + l)]) for l in range(cnt)]
                     yield
-                kk = first + 57
-                B = kk // MB
-                o0, rbase = kk - B * MB, P * ((B + NB - 3) % NB)
-                if dbl:
-                    out[t, p, c] = [(temper(ring[rbase + spill(o0 + 2 * l)]), temper(ring[rbase + spill(o0 + 2 * l + 1)]))
-                                    for l in range(cnt)]
-                else:
-                    out[t, p, c] = [temper(ring[rbase + spill(o0 + l)]) for l in range(cnt)]
-                yield
-                c += NOUT
-                while p < planes and c >= nchunk:
-                    c -= nchunk
-                    p += 1
             kpos += W
         gen_need[ow] = 0xFFFFFFFF
 
@@ -174,16 +169,16 @@ def run_model(n, planes, t0, t1, key, pos0, seed, NR, NOUT=7, PUB=4):
     return out, keys
 
 
-@pytest.mark.parametrize("NR", [1, 2])
+@pytest.mark.parametrize("NOUT,NEED_EVERY", [(3, 2), (7, 2), (3, 1)])
 @pytest.mark.parametrize("n,planes", [(100, 2), (576, 2), (300, 6), (250, 3)])
-def test_generator_protocol_model(NR, n, planes):
+def test_generator_protocol_model(NOUT, NEED_EVERY, n, planes):
     T = 4
     for seed in range(2):
         rs = np.random.RandomState(seed + 11)
         rs.uniform(size=(seed * 37) % 500)          # start mid-block (pos != 624)
         st = rs.get_state()
         key, pos = [int(x) for x in st[1]], int(st[2])
-        out, keys = run_model(n, planes, 1, T, key, pos, seed, NR)
+        out, keys = run_model(n, planes, 1, T, key, pos, seed, NOUT=NOUT, NEED_EVERY=NEED_EVERY)
         W = n * (planes // 2 * 3 + (planes & 1) * 2)
         nchunk = (n + 63) // 64
         for t in range(1, T + 1):

@@ -65,6 +65,18 @@ def workload(name, rank):
     raise SystemExit(f"unknown config {name}")
 
 
+def latest_profile(name):
+    """The newest round's copy of a measured file under profiles/r<NN>/ (None if absent)."""
+    pdir = os.path.join(ROOT, "profiles")
+    rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r") and d[1:].isdigit()), reverse=True) \
+        if os.path.isdir(pdir) else []
+    for d in rounds:
+        f = os.path.join(pdir, d, name)
+        if os.path.exists(f):
+            return f
+    return None
+
+
 def cpu_model():
     """The host CPU's model name (/proc/cpuinfo), or the platform's processor string."""
     try:
@@ -328,8 +340,8 @@ def main(argv=None):
     mt_w = window("mt19937") if args.rng == "philox" and not args.no_mt else None
 
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "r03", f"traffic_{args.config}.json")
-    if os.path.exists(tfile) and args.rng == "philox":
+    tfile = latest_profile(f"traffic_{args.config}.json")
+    if tfile and args.rng == "philox":
         # measured HBM bytes per agent-step (rocprofv3 PMC passes of this same command)
         traffic = json.load(open(tfile))["bytes_per_agent_step"] * step_agents
     if rank == 0:
@@ -352,7 +364,8 @@ def main(argv=None):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "time_base": "HIP events around the K timed iterations (device time per iteration)",
                          "achieved_wall": achieved_wall, "frac_wall": achieved_wall / HBM_PEAK_GBS,
-                         "traffic_unit": "bytes per iteration (all replicas), from profiles/r03/traffic_*.json",
+                         "traffic_unit": "bytes per iteration (all replicas), from "
+                                         + (os.path.relpath(tfile, ROOT) if tfile else "no PMC traffic file"),
                          "traffic_gbs": (traffic / per_step_dev_s / 1e9) if traffic else None,
                          "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
                          "kernel": (f"spgg_step_kernel, {resident} concurrent launches per iteration "

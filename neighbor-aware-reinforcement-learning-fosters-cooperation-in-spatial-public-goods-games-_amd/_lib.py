@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 GEN_ERR_SPIN = 1
 STATE_REPUTATION, STATE_ACTION = 0, 1

@@ -74,7 +74,7 @@ struct TileArgs {
   uint8_t* S_out;         // S_{t+1}
   const void* R_in;       // f64, or int8 units of rep_unit (compact reputation)
   void* R_out;
-  double* Q;              // [rep][n][QW], IN PLACE: after TD of t-1, before its NI term
+  double* Q;              // [rep][state plane s][n][QW/2], IN PLACE: after TD of t-1, before its NI term
   double* md;             // [rep][n], IN PLACE: max(0, max_diff) of iteration t-1
   const double* pub_in;   // border records of iteration t-1 (ring recompute reads them)
   double* pub_out;        // border records of iteration t
@@ -586,27 +586,38 @@ __device__ __forceinline__ int draw_table1(const TileArgs& a, int rep, int g, in
 
 typedef double vd2 __attribute__((ext_vector_type(2)));
 
+// Q in state planes (spgg_abi.h): a replica's table is [s][n][QH] -- plane s holds every
+// agent's row s, (Q[s,0], Q[s,1]) (Double-Q: then q_table_2's row s).  An iteration
+// changes at most the rows of its own state and of the pending NI entry (the state of
+// t-1), mostly one and the same, so the other plane's lines stay clean in the caches and
+// are not written back (the (L,L,2,2) layout dirtied every agent's whole 32 bytes).
+// vd2 index of agent g's row s: (s * n + g) * (QH / 2).
 template <int QB>
-__device__ __forceinline__ void load_q(const double* Qr, uint32_t agent, double (&q)[4],
+__device__ __forceinline__ void load_q(const double* Qr, uint32_t n, uint32_t agent, double (&q)[4],
                                        double (&qb)[QB ? 4 : 1]) {
-  const vd2* qp = at(reinterpret_cast<const vd2*>(Qr), agent * (QB ? 4 : 2));
-  const vd2 q01 = qp[0], q23 = qp[1];
+  const vd2* q0 = at(reinterpret_cast<const vd2*>(Qr), agent * (QB ? 2 : 1));
+  const vd2* q1 = at(reinterpret_cast<const vd2*>(Qr), (n + agent) * (QB ? 2 : 1));
+  const vd2 q01 = q0[0], q23 = q1[0];
   q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
   if constexpr (QB) {
-    const vd2 b01 = qp[2], b23 = qp[3];
+    const vd2 b01 = q0[1], b23 = q1[1];
     qb[0] = b01.x; qb[1] = b01.y; qb[2] = b23.x; qb[3] = b23.y;
   }
 }
 
+// Store the rows of `rows` (bit s: row s changed).
 template <int QB>
-__device__ __forceinline__ void store_q(double* Qr, uint32_t agent, const double (&q)[4],
-                                        const double (&qb)[QB ? 4 : 1]) {
-  vd2* qo = at(reinterpret_cast<vd2*>(Qr), agent * (QB ? 4 : 2));
-  qo[0] = vd2{q[0], q[1]};
-  qo[1] = vd2{q[2], q[3]};
-  if constexpr (QB) {
-    qo[2] = vd2{qb[0], qb[1]};
-    qo[3] = vd2{qb[2], qb[3]};
+__device__ __forceinline__ void store_q(double* Qr, uint32_t n, uint32_t agent, const double (&q)[4],
+                                        const double (&qb)[QB ? 4 : 1], uint32_t rows = 3u) {
+  vd2* q0 = at(reinterpret_cast<vd2*>(Qr), agent * (QB ? 2 : 1));
+  vd2* q1 = at(reinterpret_cast<vd2*>(Qr), (n + agent) * (QB ? 2 : 1));
+  if (rows & 1u) {
+    q0[0] = vd2{q[0], q[1]};
+    if constexpr (QB) q0[1] = vd2{qb[0], qb[1]};
+  }
+  if (rows & 2u) {
+    q1[0] = vd2{q[2], q[3]};
+    if constexpr (QB) q1[1] = vd2{qb[2], qb[3]};
   }
 }
 
@@ -730,7 +741,8 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, int 
 // owner writes the next ones); Q, max_diff and |alpha*td'| IN PLACE (an
 // agent's entries are read and written only by its owner; the ring recompute
 // reads the owner's border record instead), border records ping-pong.  Per
-// agent-step HBM/Infinity-Cache traffic: Q 32 B read + 32 B written, md 8 + 8,
+// agent-step HBM/Infinity-Cache traffic: Q 32 B read + 16 B written (the changed state
+// plane's row; 32 when the NI row and the TD row differ), md 8 + 8,
 // atd 4 + 4, S/R ~5 B, border records ~6 B; the working set of cfg3 (~235 MB)
 // stays within the 256 MB Infinity Cache (a ping-ponged Q alone was 270 MB).
 //
@@ -878,7 +890,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         md_own[u] = 0.0;
         atd_own[u] = 0.f;
       } else {
-        load_q<QB>(Qr, g, q[u], qb[u]);
+        load_q<QB>(Qr, (uint32_t)n, g, q[u], qb[u]);
       }
       r += dr;
       c += dc;
@@ -1026,7 +1038,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
-      store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
+      store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u]);
       *at(mdr, agent_of(rc[u])) = md_own[u];
       *at(atdr, agent_of(rc[u])) = atd_own[u];
       *at(Sout, agent_of(rc[u])) = sSv[(r + HS) * ly.sw + (c + HS)];
@@ -1071,6 +1083,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   // value slots (-> slot t-1): red 0-3 sum Q, 4-7 sum Q over prev C; the NI percent
   // (pct_t1) is reduced with phase 1b's values
   float pct_t1 = 0.f;
+  uint32_t ni_rows = 0;  // 2 bits per slot: the Q row (state plane) the NI term of t-1 changed
   {
     double v[8];
     float pct = 0.f;
@@ -1103,6 +1116,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
             q[u][k] = __builtin_fma(m, nu, q[u][k]);
             if constexpr (QB) qb[u][k] = __builtin_fma(m, nu, qb[u][QB ? k : 0]);  // both tables (spgg.py:496-502)
           }
+          ni_rows |= (1u << (e >> 1)) << (2 * u);
           // NI percent (spgg.py:512; x100 applied to the workgroup total), in f32:
           // a history mean (tolerance 1e-5), each term a ratio in [0, 1]
           const float anu = fabsf((float)nu);
@@ -1122,7 +1136,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
-    for (int u = 0; u < APT; ++u) store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);
+    for (int u = 0; u < APT; ++u) store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u]);
   }
   // the ring cells' border records (landed during phase 1a) to LDS for phase 1c:
   // held in registers across phase 1b they cost the occupancy of a fifth wave
@@ -1293,7 +1307,9 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const float atd = td_update<ALG, RNG>(a, hp, rep, agent_of(rc[u]), t, pkey, eps_t, eps53, diag_on, rew, so,
                                             act, sn, q[u], qb[u], &rn0, &rn1);
       if (diag_on && !(SPGG_ABLATE & (256 | 2048))) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
-      if (!(SPGG_ABLATE & 2048)) store_q<QB>(Qr, agent_of(rc[u]), q[u], qb[u]);  // the whole row pair
+      // the rows this launch changed: the TD row (so) and the NI row of t-1 (phase 1a)
+      if (!(SPGG_ABLATE & 2048))
+        store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u], ((ni_rows >> (2 * u)) & 3u) | (1u << so));
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -1492,14 +1508,15 @@ __global__ __launch_bounds__(kBlock) void spgg_publish_init_kernel(TileArgs a) {
   const int r = y - ty * a.TH, c = x - tx * a.TW;
   const int th = min(a.TH, L - ty * a.TH), tw = min(a.TW, L - tx * a.TW);
   if (!spgg_impl::is_border(r, c, th, tw, HA)) return;
-  const double* Q = a.Q + (rb + g) * (QB ? 8 : 4);
+  constexpr int QH = QB ? 4 : 2;  // doubles per agent and state plane (load_q)
+  const double* Q = a.Q + rb * 2 * QH + ((size_t)s1 * a.n + g) * QH;  // row s_1
   double* rec = a.pub_out + (size_t)(rep * a.tiles_per_rep + ty * a.tiles_x + tx) * PF * a.PB +
                 spgg_impl::border_slot(r, c, th, tw, HA);
-  rec[0] = Q[2 * s1];
-  rec[a.PB] = Q[2 * s1 + 1];
+  rec[0] = Q[0];
+  rec[a.PB] = Q[1];
   if constexpr (QB) {
-    rec[2 * a.PB] = Q[4 + 2 * s1];
-    rec[3 * a.PB] = Q[4 + 2 * s1 + 1];
+    rec[2 * a.PB] = Q[2];
+    rec[3 * a.PB] = Q[3];
   }
   rec[(PF - 1) * a.PB] = 0.0;
 }

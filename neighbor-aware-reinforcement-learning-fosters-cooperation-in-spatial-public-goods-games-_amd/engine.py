@@ -117,6 +117,22 @@ class ReplicaParams:
         return None
 
 
+def to_state_planes(*tables) -> np.ndarray:
+    """One replica's Q buffer (spgg_abi.h) from its (L, L, 2, 2) table(s): plane s holds every
+    agent's row s -- (2, n, 2), or for Double-Q's two tables (2, n, 4) with q_table_1's row
+    then q_table_2's -- so a launch writes back only the rows it changed."""
+    rows = [np.asarray(t, dtype=np.float64).reshape(-1, 2, 2) for t in tables]   # (n, s, a)
+    return np.stack([np.concatenate([r[:, s, :] for r in rows], axis=1) for s in range(2)])
+
+
+def from_state_planes(buf: np.ndarray, L: int, double_q: bool = False):
+    """The (L, L, 2, 2) table(s) of one replica's Q buffer (inverse of to_state_planes)."""
+    planes = np.asarray(buf).reshape(2, L * L, 4 if double_q else 2)
+    tabs = [np.ascontiguousarray(planes[:, :, 2 * i:2 * i + 2].transpose(1, 0, 2)).reshape(L, L, 2, 2)
+            for i in range(2 if double_q else 1)]
+    return tuple(tabs)
+
+
 def epsilon_table(eps0, decay, emin, n):
     """eps in effect at iterations 1..n (index t), decayed after every step (algorithms.py:42)."""
     out = np.empty(n + 1)
@@ -262,10 +278,9 @@ class BatchEngine:
         if self.double_q:
             if any(s.tables is None for s in self.init):
                 raise ValueError("double_qlearning needs both initial tables (InitState.tables)")
-            Q0 = np.stack([np.concatenate([np.asarray(t, dtype=np.float64).reshape(n, 4) for t in s.tables],
-                                          axis=1) for s in self.init])
+            Q0 = np.stack([to_state_planes(*s.tables) for s in self.init])
         else:
-            Q0 = np.stack([np.asarray(s.Q, dtype=np.float64).reshape(n, 4) for s in self.init])
+            Q0 = np.stack([to_state_planes(s.Q) for s in self.init])
         self.S = torch.zeros((2, R, n), dtype=u8, device=d)
         self.S[0].copy_(torch.from_numpy(S0))
         units = [p.rep_unit() for p in self.reps]
@@ -273,7 +288,7 @@ class BatchEngine:
                          and os.environ.get("SPGG_REP_F64", "0") != "1")
         self.rep_units = np.array([u if u is not None else 1.0 for u in units])
         self.Rep = torch.zeros((2, R, n), dtype=torch.int8 if self.rep_int8 else f64, device=d)
-        # Q updated in place (reference layout (L,L,2,2) per replica)
+        # Q updated in place, in state planes per replica (spgg_abi.h; to_state_planes)
         self.Qb = torch.from_numpy(np.ascontiguousarray(Q0)).to(d)
         # pending NI record, in place: max(0, max_diff) and |alpha*td'| (diagnostic)
         self.md = torch.zeros((R, n), dtype=f64, device=d)
@@ -585,11 +600,11 @@ class BatchEngine:
         else:   # S_{last+1}, R_{last+1}; Q finalized by the flush launch last+1
             cur = last & 1
         L = self.L
-        Qk = self.Qb[k].cpu().numpy()
+        tabs = from_state_planes(self.Qb[k].cpu().numpy(), L, self.double_q)
         if self.double_q:   # q_table = mean of the two tables (algorithms.py:262-266)
-            Q = ((Qk[:, :4] + Qk[:, 4:]) / 2).reshape(L, L, 2, 2)
+            Q = (tabs[0] + tabs[1]) / 2
         else:
-            Q = Qk.reshape(L, L, 2, 2)
+            Q = tabs[0]
         R = self._rep_host(cur)[k].reshape(L, L)
         S = (self.S[cur, k].cpu().numpy() & 1).reshape(L, L).astype(np.int64)
         return Q, R, S
@@ -598,8 +613,7 @@ class BatchEngine:
         """Double-Q: (q_table_1, q_table_2) of replica k after the run."""
         if not self.double_q:
             raise ValueError("final_tables: not a double_qlearning engine")
-        Qk = self.Qb[k].cpu().numpy()
-        return Qk[:, :4].reshape(self.L, self.L, 2, 2).copy(), Qk[:, 4:].reshape(self.L, self.L, 2, 2).copy()
+        return from_state_planes(self.Qb[k].cpu().numpy(), self.L, True)
 
     def _rep_host(self, buf):
         """R plane `buf` of every replica as float64 (exact k*unit in compact mode)."""

@@ -47,3 +47,24 @@ def test_resident_groups_fit_the_budget():
     for R in (126, 150, 210, 315, 420, 1000):
         w, g, r = plan_groups(R, 200, per_rep(200), BUDGET)
         assert r * -(-R // g) * per_rep(200) <= BUDGET * 1.05, (R, w, g, r)
+
+
+@pytest.mark.parametrize("double_q", [False, True])
+def test_state_plane_layout_round_trip(double_q):
+    """The Q buffer's state planes (spgg_abi.h): plane s holds every agent's row s, and the
+    conversion back gives the reference's (L, L, 2, 2) table(s) bit for bit."""
+    import numpy as np
+    from spgg_amd.engine import from_state_planes, to_state_planes
+    L = 5
+    rs = np.random.RandomState(3)
+    tabs = [rs.uniform(-0.01, 0.01, size=(L, L, 2, 2)) for _ in range(2 if double_q else 1)]
+    buf = to_state_planes(*tabs)
+    assert buf.shape == (2, L * L, 4 if double_q else 2)
+    y, x, s = 3, 1, 1
+    assert np.array_equal(buf[s, y * L + x, :2], tabs[0][y, x, s])
+    if double_q:
+        assert np.array_equal(buf[s, y * L + x, 2:], tabs[1][y, x, s])
+    back = from_state_planes(buf.reshape(-1), L, double_q)
+    assert len(back) == len(tabs)
+    for a, b in zip(back, tabs):
+        assert np.array_equal(a, b)

@@ -189,10 +189,10 @@ def _cpu_job(job):
 FULL_RUN_ITERS = {"cfg2": 10000, "cfg3": 10000, "cfg4": 10000, "cfg5": 100000, "run100": 100001}
 
 
-def full_run(L, M2, state, reps, rng, streams, T, offset):
+def full_run(L, M2, state, reps, rng, streams, T, offset, turn=256):
     """The configuration's whole run (BASELINE.json iterations) as a user runs it:
     BatchEngine.run() -- absorbing replicas, group retirement, host syncs every 256
-    iterations, the final flush -- timed from the first launch to the flush."""
+    iterations (`turn`), the final flush -- timed from the first launch to the flush."""
     import numpy as np
     import torch
     from spgg_amd.engine import BatchEngine
@@ -201,7 +201,7 @@ def full_run(L, M2, state, reps, rng, streams, T, offset):
     try:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.run(snapshots=False)
+        eng.run(chunk=turn, snapshots=False)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         stop = eng.stopped

@@ -48,7 +48,8 @@ using namespace spgg;
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
 //   16 = no workgroup totals (final barrier + epilogue), 512 = no per-agent Q / md / atd loads
-//   (synthetic values), 2048 = no per-agent Q / md / atd stores, 128 = memory only (the owned loads,
+//   (synthetic values), 2048 = no per-agent Q / md / atd stores, 4096 = Q plane 0 read only (plane 1's
+//   entries copied from it), 128 = memory only (the owned loads,
 //   staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
@@ -597,7 +598,7 @@ __device__ __forceinline__ void load_q(const double* Qr, uint32_t n, uint32_t ag
                                        double (&qb)[QB ? 4 : 1]) {
   const vd2* q0 = at(reinterpret_cast<const vd2*>(Qr), agent * (QB ? 2 : 1));
   const vd2* q1 = at(reinterpret_cast<const vd2*>(Qr), (n + agent) * (QB ? 2 : 1));
-  const vd2 q01 = q0[0], q23 = q1[0];
+  const vd2 q01 = q0[0], q23 = (SPGG_ABLATE & 4096) ? q01 : q1[0];  // 4096: one plane's reads only
   q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
   if constexpr (QB) {
     const vd2 b01 = q0[1], b23 = q1[1];
@@ -2147,6 +2148,13 @@ int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
 // one agent per thread, 8 replicas (320 tiles, M=2) 16.2 -> 17.0, one L=1000
 // replica (1000 tiles) 28.1 -> 53.9.  SPGG_APT=1 / =<max> forces either.
 constexpr long long kSmallBatchTiles = 128;
+// Below this many 1024-agent tiles, two agents per thread (20 x 25 tiles, compile-time width
+// 20: where 20 divides L >= 60) -- twice the workgroups of half the length (round 4, L=200,
+// us/step at 1 / 2 replica groups, profiles/r04/plan_sweep.txt: one replica 8.38 vs 10.65 at
+// one agent per thread; run100 7.78 vs 9.34; 8 replicas M=2 action 12.43 vs 14.17 at four
+// agents per thread; 16 replicas 13.89 vs 14.18 (M=1); 32 replicas 23.90 vs 23.07 and one
+// L=1000 replica, 1000 tiles, 33.4 vs 26.3: four agents per thread from here on).
+constexpr long long kTwoPerThreadTiles = 800;
 
 // MT19937 generator layout (spgg_mt_chains).  One chain generates a replica's draws at
 // ~200 ns per 227 words (measured: 119-215 ns with the steps running), i.e. ~W/227*0.2 us
@@ -2526,9 +2534,10 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   // the step kernel addresses a replica's arrays with 32-bit byte offsets (Q: qw doubles per agent)
   if ((long long)cfg->L * cfg->L * spgg_impl::qw_of(cfg->algorithm) * 8 > 0xFFFFFFFFLL)
     return create_fail(SPGG_E_ARG, "spgg_create: a replica's Q table exceeds 4 GiB (32-bit offsets)");
-  // Agents per thread: the operator's maximum (tiles of up to 1024 agents), or
-  // one for a batch that would launch fewer than kSmallBatchTiles workgroups
-  // (4x the workgroups, each a quarter as long).  Decided from the WHOLE batch
+  // Agents per thread: the operator's maximum (tiles of up to 1024 agents); two for a
+  // batch of fewer than kTwoPerThreadTiles such tiles where 20 x 25 tiles fit L; else one
+  // for a batch that would launch fewer than kSmallBatchTiles workgroups (4x the
+  // workgroups, each a quarter as long).  Decided from the WHOLE batch
   // (batch_reps), so the replica groups of one batch share one tiling: their
   // border-record and history-record strides must agree.  SPGG_APT = 1 / max forces either.
   const int apt_max = spgg_impl::apt_of(cfg->algorithm);
@@ -2545,6 +2554,8 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
       else
         return create_fail(SPGG_E_ARG, std::string("SPGG_APT=") + e + ": expected 1, 2 or max (" +
                                            std::to_string(apt_max) + " agents per thread for this operator)");
+    } else if (tiles4 < kTwoPerThreadTiles && apt_max > 2 && cfg->L % 20 == 0 && cfg->L >= 60) {
+      apt = 2;
     } else if (tiles4 < kSmallBatchTiles) {
       apt = 1;
     }

@@ -179,8 +179,11 @@ def plan_groups(R: int, L: int, bytes_per_replica: int, cache_bytes: int, stream
     MI355X, profiles/r02/streams_by_batch.txt): >= 2400 tiles 2 groups (105 x L=200:
     2 groups 64.8 us/step, 3 66.5, 4 75.5; 70 replicas 46.0 / 47.0; cache-blocked 210
     and 420 replicas 131.9 / 256.5 us at 2 per wave vs 136.8 / 265.3 at 3), 1200-2400
-    tiles 3 groups (35 replicas 27.4 vs 28.2 at 2, 52 replicas 36.2 vs 37.8), fewer
-    tiles one group (cross-stream ordering costs more than it hides); never 4 at once
+    tiles 3 groups (35 replicas 27.4 vs 28.2 at 2, 52 replicas 36.2 vs 37.8), 300-1200
+    tiles 2 groups (round 4, two agents per thread below 800 tiles: 8 x L=200 M=1 10.98 vs
+    11.47 us/step, M=2 action 12.43 vs 13.89; 16 replicas 13.89 vs 15.78, 18.06 vs 20.90;
+    profiles/r04/plan_sweep.txt), fewer tiles one group (4 replicas M=1 9.03 vs 9.36:
+    cross-stream ordering costs more than it hides); never 4 at once
     (more streams than the 4 hardware queues serialise).  A batch whose state
     exceeds the Infinity-Cache budget is split into `waves` of groups that fit; the
     `resident` groups of a wave run concurrently and the next wave's groups queue
@@ -193,7 +196,7 @@ def plan_groups(R: int, L: int, bytes_per_replica: int, cache_bytes: int, stream
         tw = min(L, 40)
         tiles = -(-L // tw) * -(-L // min(L, 25))
         tpw = R / waves * tiles
-        per_wave = 2 if tpw >= 2400 else (3 if tpw >= 1200 else 1)
+        per_wave = 2 if tpw >= 2400 else (3 if tpw >= 1200 else (2 if tpw >= 300 else 1))
         per_wave = int(max(1, min(per_wave, -(-R // waves))))
         streams = per_wave * waves if waves > 1 else per_wave
     groups = max(1, min(int(streams), R))
@@ -462,6 +465,7 @@ class BatchEngine:
             for h in self._own_streams:
                 self.lib.spgg_stream_destroy(h)
             self._own_streams = []
+            self._loop = None
 
     def __del__(self):
         try:
@@ -526,16 +530,9 @@ class BatchEngine:
         return n_steps
 
     def all_stopped(self) -> bool:
-        """Host check of the absorbing stops (a sync).  A group whose replicas have all
-        stopped is retired: its later launches would only stage loads and exit (every
-        workgroup of an absorbed replica returns before computing), so they are skipped."""
-        self.stopped = self.stop_iter.cpu().numpy().astype(np.int64)
-        self.check_status()
-        if self.skip_dead:
-            for g in self.groups:
-                if g["live"] and np.all(self.stopped[g["r0"]:g["r1"]] != 0):
-                    g["live"] = False
-        return bool(np.all(self.stopped != 0))
+        """Host check of the absorbing stops (a sync of the current stream); retires groups
+        whose replicas have all stopped (_note_stops)."""
+        return self._note_stops(self.stop_iter.cpu().numpy())
 
     def flush(self):
         """Apply the deferred NI term of the last executed iteration (once, at the end)."""
@@ -545,29 +542,84 @@ class BatchEngine:
         self._enqueue(lambda g, s: C.check(self.lib.spgg_flush(g["ctx"], tl, s), g["ctx"], "spgg_flush"))
         self._flushed = True
 
+    def _note_stops(self, stop) -> bool:
+        """Absorbing stops as of some enqueued iteration: retire groups whose replicas have all
+        stopped (their later launches would only stage loads and exit), raise on a generator
+        error; True once every replica has stopped."""
+        self.stopped = np.asarray(stop).astype(np.int64)
+        self.check_status()
+        if self.skip_dead:
+            for g in self.groups:
+                if g["live"] and np.all(self.stopped[g["r0"]:g["r1"]] != 0):
+                    g["live"] = False
+        return bool(np.all(self.stopped != 0))
+
+    def _loop_stream(self):
+        """The stream run() orders its turns, stop-flag copies and host syncs on, instead of the
+        legacy null stream -- which every blocking stream (the CU-masked group and MT19937
+        generator streams) synchronises with, so a host sync there drained the generator's
+        queued chunks at every turn.  Replica groups: group 0's stream (a fifth stream would
+        share one of the 4 hardware queues: cfg3 MT19937 whole run 92.6 us/iter on a stream of
+        its own, 78.7 on the null stream, 71.9 on group 0's); one group: a library-made
+        stream (cfg5 MT19937 whole run 27.4 vs 32.3 on the null stream, cfg2 10.0 vs 11.1).
+        profiles/r04/turns_and_loop_stream.txt."""
+        if self.G > 1:
+            return self.streams[0]
+        if getattr(self, "_loop", None) is None:
+            h = ctypes.c_void_p()
+            C.check(self.lib.spgg_stream_create(self.dev.index, ctypes.byref(h)), None, "spgg_stream_create")
+            self._own_streams.append(h.value)
+            self._loop = torch.cuda.ExternalStream(h.value, device=self.dev)
+        return self._loop
+
     def run(self, chunk: int = 256, snapshots: bool = True, png: bool = False,
             progress: Optional[Callable[[int], None]] = None):
-        """Execute iterations until `iterations` or every replica is absorbed."""
+        """Execute iterations until `iterations` or every replica is absorbed.
+
+        Turns of `chunk` iterations.  The absorbing-stop check of a turn is an asynchronous
+        copy of the stop flags; the host reads it one turn later (the device never idles at
+        a turn boundary; absorbed replicas' launches return at once, so running on past an
+        absorbing stop changes no result).  Snapshot iterations sync."""
         stops = set()
         if snapshots:
             stops |= {i for i in SNAPSHOT_ITERS if i <= self.T}
         if png:
             stops |= {i + 1 for i in PNG_ITERS if i + 1 <= self.T + 1}
-        while self.t <= self.T:
-            if self.t in stops:
-                self._capture(self.t, snapshots and self.t in SNAPSHOT_ITERS,
-                              png and (self.t - 1) in PNG_ITERS)
-            nxt = min([s for s in stops if s > self.t] + [self.t + chunk, self.T + 1])
-            self.step(nxt - self.t)
-            if progress:
-                progress(self.t - 1)
-            if self.all_stopped():
-                break
-        if png and self.t in stops and (self.t - 1) in PNG_ITERS:
-            self._capture(self.t, False, True)
-        self.flush()
+        caller = torch.cuda.current_stream(self.dev)
+        loop = self._loop_stream()
+        loop.wait_stream(caller)
+        flags = torch.empty((2, self.R), dtype=torch.int32, pin_memory=True)
+        pending = []   # (event, slot) of the stop-flag copies in flight (<= 2: this turn's, the last one's)
+        turn = 0
+        done = False
+        with torch.cuda.stream(loop):
+            while self.t <= self.T and not done:
+                if self.t in stops:
+                    self._capture(self.t, snapshots and self.t in SNAPSHOT_ITERS,
+                                  png and (self.t - 1) in PNG_ITERS)
+                    pending = []   # (_capture synchronised the stream)
+                    done = self._note_stops(self.stop_iter.cpu().numpy())
+                    if done:
+                        break
+                nxt = min([s for s in stops if s > self.t] + [self.t + chunk, self.T + 1])
+                self.step(nxt - self.t)
+                if progress:
+                    progress(self.t - 1)
+                slot, turn = turn & 1, turn + 1
+                flags[slot].copy_(self.stop_iter, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(loop)
+                pending.append((ev, slot))
+                if len(pending) == 2:   # the previous turn's flags (this turn is still running)
+                    ev0, s0 = pending.pop(0)
+                    ev0.synchronize()
+                    done = self._note_stops(flags[s0].numpy())
+            if png and self.t in stops and (self.t - 1) in PNG_ITERS:
+                self._capture(self.t, False, True)
+            self.flush()
+        caller.wait_stream(loop)
         torch.cuda.synchronize(self.dev)
-        self.stopped = self.stop_iter.cpu().numpy().astype(np.int64)
+        self._note_stops(self.stop_iter.cpu().numpy())
 
     def _capture(self, t, snap, png):
         """Host copies of S_t / R_t at iteration start (spgg.py:397-402) and of the

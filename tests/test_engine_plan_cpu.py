@@ -17,7 +17,9 @@ def per_rep(L, qw=4, rsz=1):  # engine.state_bytes_per_replica for Q-learning, i
     (52, 200, (1, 3, 3)),      # 2080 tiles: 3 groups
     (35, 200, (1, 3, 3)),
     (1, 200, (1, 1, 1)),       # cfg2
-    (8, 200, (1, 1, 1)),       # cfg4-sized batch: one group
+    (8, 200, (1, 2, 2)),       # cfg4-sized batch (320 tiles): two groups
+    (16, 200, (1, 2, 2)),
+    (4, 200, (1, 1, 1)),       # 160 tiles: one group
     (126, 200, (2, 4, 2)),     # past the cache: 2 waves of 2 resident groups
     (210, 200, (2, 4, 2)),
     (420, 200, (4, 8, 2)),     # 4 waves of cfg3-sized work

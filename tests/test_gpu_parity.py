@@ -398,17 +398,22 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
 
 
 @pytest.mark.parametrize("rng", ["philox", "mt19937"])
-def test_groups_straddling_small_batch_threshold_share_one_tiling(rng):
-    """7 x L=200 over 2 streams: groups of 4 (160 1000-agent tiles) and 3 replicas (120,
-    under the 128-tile small-batch threshold on its own).  The tiling is chosen from the
-    whole batch, so both groups use the same tile shape, border-record and history-record
-    strides, and the results equal the one-stream run's bit for bit."""
+@pytest.mark.parametrize("n_reps,tile", [(24, (40, 25)), (7, (20, 25))])
+def test_groups_straddling_small_batch_threshold_share_one_tiling(rng, n_reps, tile):
+    """L=200 batches over 2 streams whose groups alone would get another tiling: 24 replicas
+    (960 1000-agent tiles: four agents per thread) in groups of 12 (480 tiles each, under the
+    800-tile two-agents-per-thread threshold on its own), and 7 replicas (280 tiles: two
+    agents per thread) in groups of 4 and 3 (120 tiles, once under the 128-tile threshold).
+    The tiling is chosen from the whole batch, so both groups use the same tile shape,
+    border-record and history-record strides, and the results equal the one-stream run's
+    bit for bit."""
     L, T = 200, 30
-    reps = [_runner_params(r=2.5 + 0.4 * s, influence_factor=0.5 * (s % 3), seed=90 + s) for s in range(7)]
+    reps = [_runner_params(r=2.5 + 0.4 * (s % 7), influence_factor=0.5 * (s % 3), seed=90 + s)
+            for s in range(n_reps)]
     res = {}
     for G in (1, 2):
         eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=G)
-        assert eng.G == G and eng.tile == (40, 25)
+        assert eng.G == G and eng.tile == tile
         assert len({eng._layout(g["ctx"]) for g in eng.groups}) == 1
         eng.run(snapshots=False)
         res[G] = ([eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy())
@@ -494,14 +499,21 @@ def test_spgg_dropin_max_agents_per_thread(name, tmp_path, monkeypatch):
 
 
 def test_one_agent_per_thread_mode_selectable(monkeypatch):
-    """Default: one agent per thread (tiles <= 256 agents) for a batch of fewer than 128
-    1000-agent tiles (one L=200 replica), 1000-agent tiles above (8 replicas); SPGG_APT
-    forces either."""
+    """Default: two agents per thread (20 x 25 tiles) for a batch of fewer than 800
+    1000-agent tiles where 20 divides L (one or 8 L=200 replicas), 1000-agent tiles above
+    (24 replicas), one agent per thread (tiles <= 256 agents) for fewer than 128 tiles when
+    20 does not divide L (L=50); SPGG_APT forces any."""
     eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
-    assert eng.tile[0] * eng.tile[1] <= 256
+    assert eng.tile == (20, 25)
     eng.close()
     eng = BatchEngine(200, 5, [_runner_params(seed=s) for s in range(8)], use_second_order=False, rng="philox")
+    assert eng.tile == (20, 25)
+    eng.close()
+    eng = BatchEngine(200, 5, [_runner_params(seed=s) for s in range(24)], use_second_order=False, rng="philox")
     assert eng.tile == (40, 25)
+    eng.close()
+    eng = BatchEngine(50, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")
+    assert eng.tile[0] * eng.tile[1] <= 256
     eng.close()
     _force_apt(monkeypatch, "max")
     eng = BatchEngine(200, 5, [_runner_params(seed=0)], use_second_order=False, rng="philox")

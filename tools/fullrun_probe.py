@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3000)
     ap.add_argument("--after-bench", action="store_true")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--turn", type=int, default=256, help="iterations between host syncs (BatchEngine.run chunk)")
     a = ap.parse_args()
     import torch
     import bench
@@ -30,8 +31,8 @@ def main():
         torch.cuda.synchronize()
         eng.close()
     for i in range(a.repeat):
-        r = bench.full_run(L, M2, state, reps, a.rng, None, a.iters, 0)
-        print(f"{a.config} {a.rng} after_bench={a.after_bench} run {i}: {r['seconds'] / a.iters * 1e6:.2f} us/iter "
+        r = bench.full_run(L, M2, state, reps, a.rng, None, a.iters, 0, a.turn)
+        print(f"{a.config} {a.rng} turn={a.turn} after_bench={a.after_bench} run {i}: {r['seconds'] / a.iters * 1e6:.2f} us/iter "
               f"({r['value']:.3g} agent-steps/s)", flush=True)
 
 

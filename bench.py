@@ -246,11 +246,15 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
     dist = None
-    # the collectives' backend: RCCL ("nccl") on the GPUs; $SPGG_DIST_BACKEND=gloo for the CPU test
-    # of this launch path (tests/test_bench_world_cpu.py), whose collectives then run on host tensors
+    # the collectives' backend: RCCL ("nccl") on the GPUs; $SPGG_DIST_BACKEND=gloo for the tests of
+    # this launch path (tests/test_bench_world_cpu.py on CPU; tests/test_gpu_launch_world2.py: two
+    # ranks sharing one GPU, which RCCL refuses), whose collectives then run on host tensors
     backend = os.environ.get("SPGG_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()   # (counts devices without initialising one)
+    if backend == "nccl" and local >= max(ndev, 1):
+        raise SystemExit(f"LOCAL_RANK {local} but {ndev} GPU(s): one rank per GPU")
+    torch.cuda.set_device(local % ndev if ndev else local)
     coll_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--rng", default="mt19937")
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=None, help="replica groups (default: the planner's)")
     args = ap.parse_args()
     import torch
     import bench
@@ -30,7 +31,7 @@ def main():
         order = order[r % len(order):] + order[:r % len(order)]
         for i in order:
             eng = BatchEngine(L, args.iters, reps, use_second_order=M2, state_representation=state, rng=args.rng,
-                              lib_path=os.path.abspath(args.libs[i]))
+                              lib_path=os.path.abspath(args.libs[i]), streams=args.streams)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             eng.run(snapshots=False)

@@ -21,13 +21,14 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--t", type=int, default=30)
+    ap.add_argument("--rng", default="philox", choices=["philox", "mt19937"])
     args = ap.parse_args()
     import torch
     import bench
     from spgg_amd.engine import BatchEngine
     desc, L, M2, state, reps = bench.workload(args.config, 0)
     lib = os.path.abspath(args.lib)
-    eng = BatchEngine(L, args.t + 5, reps, use_second_order=M2, state_representation=state, rng="philox",
+    eng = BatchEngine(L, args.t + 5, reps, use_second_order=M2, state_representation=state, rng=args.rng,
                       lib_path=lib, streams=1)
     eng.step(args.t + 2)
     torch.cuda.synchronize()

@@ -204,6 +204,22 @@ def plan_groups(R: int, L: int, bytes_per_replica: int, cache_bytes: int, stream
     return waves, groups, resident
 
 
+# Library-made streams (spgg_stream_create) are pooled per library and device and never
+# destroyed: torch's pinned-memory allocator keeps the events of a pinned buffer's copies (run()'s
+# stop flags) and queries them when it allocates again, so a stream destroyed under such an event
+# made a later engine's pinned allocation fail (hipErrorCapturedEvent).
+_STREAM_POOL: dict = {}
+
+
+def _take_stream(lib, dev_index: int) -> int:
+    free = _STREAM_POOL.setdefault((getattr(lib, "_name", id(lib)), dev_index), [])
+    if free:
+        return free.pop()
+    h = ctypes.c_void_p()
+    C.check(lib.spgg_stream_create(dev_index, ctypes.byref(h)), None, "spgg_stream_create")
+    return h.value
+
+
 class BatchEngine:
     """n_rep independent replicas of one (L, M, state) configuration on one device."""
 
@@ -339,9 +355,7 @@ class BatchEngine:
             # two streams on one queue run serialised (cfg3, a second engine in the process:
             # 80-82 us/iter on pool streams, 58.5-59 on the library's; profiles/r03/streams.txt)
             for _ in range(self.resident):
-                h = ctypes.c_void_p()
-                C.check(self.lib.spgg_stream_create(self.dev.index, ctypes.byref(h)), None, "spgg_stream_create")
-                self._own_streams.append(h.value)
+                self._own_streams.append(_take_stream(self.lib, self.dev.index))
             streams = [torch.cuda.ExternalStream(h, device=self.dev) for h in self._own_streams]
         else:
             streams = [torch.cuda.Stream(self.dev) for _ in range(self.resident)]
@@ -462,8 +476,7 @@ class BatchEngine:
         if getattr(self, "_own_streams", None):
             torch.cuda.synchronize(self.dev)
             self.streams = []
-            for h in self._own_streams:
-                self.lib.spgg_stream_destroy(h)
+            _STREAM_POOL[(getattr(self.lib, "_name", id(self.lib)), self.dev.index)].extend(self._own_streams)
             self._own_streams = []
             self._loop = None
 
@@ -566,10 +579,9 @@ class BatchEngine:
         if self.G > 1:
             return self.streams[0]
         if getattr(self, "_loop", None) is None:
-            h = ctypes.c_void_p()
-            C.check(self.lib.spgg_stream_create(self.dev.index, ctypes.byref(h)), None, "spgg_stream_create")
-            self._own_streams.append(h.value)
-            self._loop = torch.cuda.ExternalStream(h.value, device=self.dev)
+            h = _take_stream(self.lib, self.dev.index)
+            self._own_streams.append(h)
+            self._loop = torch.cuda.ExternalStream(h, device=self.dev)
         return self._loop
 
     def run(self, chunk: int = 256, snapshots: bool = True, png: bool = False,

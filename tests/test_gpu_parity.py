@@ -655,3 +655,22 @@ def test_kappa_woken_mid_run_is_refused():
         torch.cuda.synchronize()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("streams", [1, 3])
+def test_engines_in_sequence_reuse_library_streams(streams):
+    """run() copies its stop flags through a pinned buffer on a library-made stream, and torch's
+    pinned-memory allocator queries that copy's event on a later allocation: the streams outlive
+    their engine (a pool per library and device), so back-to-back engines in one process run
+    without a HIP error, and a later engine takes the earlier one's streams."""
+    import torch
+    reps = [_runner_params(r=3.0 + 0.3 * s, seed=90 + s) for s in range(3)]
+    seen = []
+    for rng in ("mt19937", "philox", "mt19937"):
+        eng = BatchEngine(20, 300, reps, use_second_order=False, rng=rng, streams=streams)
+        eng.run(chunk=64, snapshots=False)
+        flags = torch.empty((2, 3), dtype=torch.int32, pin_memory=True)   # the allocation that failed
+        seen.append(set(eng._own_streams))
+        eng.close()
+        del flags
+    assert seen[0] and seen[0] == seen[1] == seen[2]   # (the pool hands streams back last-in first-out)

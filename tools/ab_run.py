@@ -37,6 +37,7 @@ def main():
             eng.run(snapshots=False)
             torch.cuda.synchronize()
             times[args.libs[i]].append((time.perf_counter() - t0) / (eng.t - 1) * 1e6)
+            print(f"  round {r} {args.libs[i]}: {times[args.libs[i]][-1]:.2f} us/iter", flush=True)
             eng.close()
     for p in args.libs:
         print(f"{args.config} {args.rng} {os.path.basename(p):24s} median {statistics.median(times[p]):7.2f} us/iter  "

@@ -1698,10 +1698,14 @@ constexpr int kMtBlock = 227;                    // 624 - 397: words one depende
 constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
 constexpr int kGenNB = 16;                       // ring blocks
 constexpr int kGenRing = kGenPitch * (kGenNB + 1);  // + a mirror of block 0 behind the last one
-// Bound of every wait loop between the generator's waves (~0.5 s of s_sleep): a wait that
-// long means a defect.  The kernel then ends instead of hanging the GPU, and records
-// SPGG_GEN_ERR_SPIN in the context's error word, which spgg_flush / spgg_status report
-// (SPGG_E_STATE): the draws of such a run are not the reference's.
+// Progress a failed recurrence wave publishes: every output wave's wait then ends at once.
+constexpr uint32_t kGenDoneAbort = (0xffffffffu - 624u) / kMtBlock;
+// Bound of every wait loop between the generator's waves (0.2-0.5 s of s_sleep): a wait that
+// long means a defect.  The wave then records SPGG_GEN_ERR_SPIN in the context's error word,
+// which spgg_flush / spgg_status report (SPGG_E_STATE: the draws of such a run are not the
+// reference's), releases the other waves (need 0xffffffff / progress kGenDoneAbort) and
+// stops, so the kernel ends instead of hanging the GPU.  (The recurrence wave stops through its
+// last-block path: an early return there took the kernel from 51 to 74 VGPRs.)
 constexpr uint32_t kGenSpinMax = 1u << 23;
 
 // The 227 positions of a block in 4 slots of 64 lanes: slot s holds positions
@@ -1851,6 +1855,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     int t = t0;
     uint32_t key_mb = 0, key_pos = pos0;
     uint32_t b = 0;     // blocks completed
+    bool aborted = false;  // a flow-control wait ran out of its bound
     // key after iteration t (words [mb, mb+624) and pos), to the snapshot ring; then the next
     auto retire = [&]() {
       uint32_t* sn = g.snap + (size_t)(t % g.snap_slots) * g.snap_stride + (size_t)rep * 625;
@@ -1883,7 +1888,11 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       lim = m > 0xffffffffu - (kGenNB - 1) * kMtBlock ? 0xffffffffu : m + (kGenNB - 1) * kMtBlock;        \
       if (F > lim) __builtin_amdgcn_s_sleep(2);                                                           \
     }                                                                                                     \
-    if (spin == kGenSpinMax) gen_fail(g);                                                                 \
+    if (spin == kGenSpinMax) { /* this block is the last: rec_done publishes kGenDoneAbort */            \
+      gen_fail(g);                                                                                        \
+      aborted = true;                                                                                     \
+      nblk = b + 1;                                                                                       \
+    }                                                                                                     \
     GEN_FENCE();                                                                                          \
     uint32_t na[kGenSPW], nb[kGenSPW];                                                                    \
     _Pragma("unroll") for (int i = 0; i < kGenSPW; ++i) {                                                 \
@@ -1911,7 +1920,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     }
 #undef SPGG_GEN_BLOCK
   rec_done:
-    LDS_ST(gen_done[lane], b);  // (published every kGenPub blocks: the rest)
+    LDS_ST(gen_done[lane], aborted ? kGenDoneAbort : b);  // (published every kGenPub blocks: the rest)
     GEN_FENCE();
     while (t <= t1) retire();  // (the frontier covers every remaining target)
     if (last_chain) {
@@ -1953,7 +1962,11 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
           seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
           if (seen <= last) __builtin_amdgcn_s_sleep(1);
         }
-        if (spin == kGenSpinMax) gen_fail(g);
+        if (spin == kGenSpinMax) {
+          gen_fail(g);
+          LDS_ST(gen_need[ow][lane], 0xffffffffu);
+          return;
+        }
         GEN_FENCE();
         // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
         const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
@@ -2383,16 +2396,16 @@ void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t
 // one are serialised; SPGG_STREAM_MODE: 0 = hipStreamCreateWithFlags, 1 = greatest priority,
 // 2 (default) = a CU mask of every CU (a queue of its own), 3 = CU-masked and partitioned: the
 // generator on every SPGG_GEN_CU_STRIDE-th CU (default 8: 32 of 256), the groups on the rest.
-// The generator's stream (SPGG_GEN_STREAM_MODE): CU-masked streams are BLOCKING -- every
-// operation on the legacy null stream (torch's default: the engine's stream ordering and host
-// syncs) then waits for the generator's queued chunks.  For a small batch that serialises the
-// pipeline (MT19937 whole runs, plain non-blocking vs CU-masked: cfg2 11.1 vs 15.8 us/iter,
-// cfg4 16.8 vs 22.7, cfg5 32.3 vs 52.1); a batch that fills the GPU (>= 2400 tiles) runs faster
-// with the generator held to the host's 256-iteration turns than concurrently with every step
-// (cfg3 84.0 vs 99.9); profiles/r03/streams.txt.  Default: mode 2 for such batches, else 0.
-hipError_t make_stream(hipStream_t* s, bool gen, bool big_batch = false) {
+// The generator's stream (SPGG_GEN_STREAM_MODE): plain non-blocking (mode 0).  CU-masked streams
+// are BLOCKING -- every operation on the legacy null stream then waits for the generator's queued
+// chunks (round 3, when the engine synced on the null stream: cfg2 11.1 vs 15.8 us/iter, cfg5 32.3
+// vs 52.1, but cfg3 84.0 vs 99.9 in favour of the CU mask; profiles/r03/streams.txt).  Since the
+// engine's run loop left the null stream (round 4), mode 0 is the faster one at every batch size
+// (cfg3 MT19937 whole run 71.4 vs 74.1 us/iter, cfg5 36.0 vs 41.3; an idle CU-masked generator
+// stream alone slowed the steps: 59.7 vs 65.6; profiles/r04/generator_stream_modes.txt).
+hipError_t make_stream(hipStream_t* s, bool gen) {
   const char* e = getenv(gen ? "SPGG_GEN_STREAM_MODE" : "SPGG_STREAM_MODE");
-  const int mode = e ? atoi(e) : (gen && !big_batch) ? 0 : 2;
+  const int mode = e ? atoi(e) : gen ? 0 : 2;
   if (mode == 1 || mode == 4) {  // 1: greatest priority, 4: least (non-blocking)
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
@@ -2420,8 +2433,7 @@ int mt_lazy_init(spgg_ctx* c) {
   if (c->gen_done[0] && c->h_err) return SPGG_OK;
   int rc = SPGG_OK;
   if (!c->gen_stream) {
-    const long long batch = c->cfg.batch_reps > 0 ? c->cfg.batch_reps : c->cfg.n_rep;
-    rc = hip_check(c, make_stream(&c->gen_stream, true, batch * c->tiles_per_rep >= 2400), "hipStreamCreate(gen)");
+    rc = hip_check(c, make_stream(&c->gen_stream, true), "hipStreamCreate(gen)");
     if (rc) return rc;
     c->own_gen_stream = true;
   }

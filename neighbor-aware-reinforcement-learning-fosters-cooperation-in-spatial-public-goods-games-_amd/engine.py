@@ -19,6 +19,7 @@ Random streams:
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import dataclasses
 import math
@@ -204,20 +205,51 @@ def plan_groups(R: int, L: int, bytes_per_replica: int, cache_bytes: int, stream
     return waves, groups, resident
 
 
-# Library-made streams (spgg_stream_create) are pooled per library and device and never
-# destroyed: torch's pinned-memory allocator keeps the events of a pinned buffer's copies (run()'s
+# Library-made streams (spgg_stream_create) are pooled per library and device and outlive their
+# engine: torch's pinned-memory allocator keeps the events of a pinned buffer's copies (run()'s
 # stop flags) and queries them when it allocates again, so a stream destroyed under such an event
-# made a later engine's pinned allocation fail (hipErrorCapturedEvent).
-_STREAM_POOL: dict = {}
+# made a later engine's pinned allocation fail (hipErrorCapturedEvent).  They are destroyed at
+# interpreter exit, after a device sync and torch's pinned cache release, while the HIP runtime
+# (and a profiler's interception of it) is still up.
+_STREAM_POOL: dict = {}   # (library, device) -> free stream handles
+_STREAM_OWNER: dict = {}  # every live pooled stream -> (library, device)
+
+
+def _pool_key(lib, dev_index: int):
+    return (getattr(lib, "_name", id(lib)), dev_index)
 
 
 def _take_stream(lib, dev_index: int) -> int:
-    free = _STREAM_POOL.setdefault((getattr(lib, "_name", id(lib)), dev_index), [])
+    free = _STREAM_POOL.setdefault(_pool_key(lib, dev_index), [])
     if free:
         return free.pop()
     h = ctypes.c_void_p()
     C.check(lib.spgg_stream_create(dev_index, ctypes.byref(h)), None, "spgg_stream_create")
+    _STREAM_OWNER[h.value] = (lib, dev_index)
     return h.value
+
+
+def _give_streams(handles) -> None:
+    for h in handles:
+        if h in _STREAM_OWNER:   # (not yet destroyed by the exit hook)
+            lib, dev = _STREAM_OWNER[h]
+            _STREAM_POOL.setdefault(_pool_key(lib, dev), []).append(h)
+
+
+@atexit.register
+def _destroy_streams() -> None:
+    if not _STREAM_OWNER:
+        return
+    try:
+        for dev in {d for _, d in _STREAM_OWNER.values()}:
+            torch.cuda.synchronize(dev)
+        torch._C._host_emptyCache()
+    except Exception:
+        pass
+    for h, (lib, _) in list(_STREAM_OWNER.items()):
+        lib.spgg_stream_destroy(h)
+    _STREAM_OWNER.clear()
+    _STREAM_POOL.clear()
 
 
 class BatchEngine:
@@ -476,7 +508,7 @@ class BatchEngine:
         if getattr(self, "_own_streams", None):
             torch.cuda.synchronize(self.dev)
             self.streams = []
-            _STREAM_POOL[(getattr(self.lib, "_name", id(self.lib)), self.dev.index)].extend(self._own_streams)
+            _give_streams(self._own_streams)
             self._own_streams = []
             self._loop = None
 

@@ -1689,14 +1689,22 @@ constexpr int kGenSPW = 4;                       // slots of the lone recurrence
 // Blocks between two progress publications of the recurrence wave (each publication waits
 // for the wave's LDS writes: one exposed LDS round trip per period).
 constexpr int kGenPub = 4;
-static_assert(16 % kGenPub == 0, "publication period divides the unrolled block loop");
-// Chunks between two publications of an output wave's need (the recurrence may run 15 blocks,
-// 3405 words, past the smallest need; a wave's need lags its reads by < 2 x 3 x 128 words).
+
+// Chunks between two publications of an output wave's need (the recurrence may run kGenNB - 1 blocks
+// past the smallest need; a wave's need lags its reads by < 2 x 3 x 128 words).
 constexpr int kGenNeedEvery = 2;
 constexpr int kGenThreads = 64 * (1 + kGenOut);
 constexpr int kMtBlock = 227;                    // 624 - 397: words one dependency step produces
 constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
-constexpr int kGenNB = 16;                       // ring blocks
+// Ring blocks.  Not a lever: 8 or 12 (10 / 14 KB of LDS instead of 18) measured the same whole runs
+// (profiles/r04/generator_groups.txt) -- with the generator resident, the step kernel's occupancy
+// is bound by VGPRs, not LDS.
+constexpr int kGenNB = 16;
+static_assert(kGenNB == 16, "the block loop is unrolled kGenNB times");
+static_assert(kGenNB % kGenPub == 0, "publication period divides the unrolled block loop");
+// an output wave reads at most 2 x 3 x 128 - 1 words past its published need; the frontier it is
+// guaranteed to see lies (kGenNB - kGenPub) x 227 + 1 words past the smallest need
+static_assert(2 * kGenOut * 128 - 1 < (kGenNB - kGenPub) * kMtBlock + 1, "output waves' progress");
 constexpr int kGenRing = kGenPitch * (kGenNB + 1);  // + a mirror of block 0 behind the last one
 // Progress a failed recurrence wave publishes: every output wave's wait then ends at once.
 constexpr uint32_t kGenDoneAbort = (0xffffffffu - 624u) / kMtBlock;
@@ -1911,7 +1919,6 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     ++b;                                                                                                  \
     if ((U + 1) % kGenPub == 0) LDS_ST(gen_done[lane], b);                                                \
   }
-    static_assert(kGenNB == 16, "the block loop below is unrolled kGenNB times");
     for (;;) {
       SPGG_GEN_BLOCK(0) SPGG_GEN_BLOCK(1) SPGG_GEN_BLOCK(2) SPGG_GEN_BLOCK(3)
       SPGG_GEN_BLOCK(4) SPGG_GEN_BLOCK(5) SPGG_GEN_BLOCK(6) SPGG_GEN_BLOCK(7)

@@ -1958,21 +1958,27 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       const uint32_t th_hi = __builtin_amdgcn_readfirstlane((uint32_t)(th >> 26));
       const uint32_t th_lo = __builtin_amdgcn_readfirstlane((uint32_t)th & ((1u << 26) - 1u));
       const uint32_t base = kpos + plane_word0((uint32_t)g.n, p);
-      const uint32_t wstep = dbl ? 128u : 64u, wlane = dbl ? 2u * lane : (uint32_t)lane;
+      // (the chunk loop is instantiated per plane kind: the kind's branches leave the loop)
+      auto chunks = [&](auto dbl_c) -> bool {
+      constexpr bool dbl = decltype(dbl_c)::value;
+      constexpr uint32_t wstep = dbl ? 128u : 64u;
+      const uint32_t wlane = dbl ? 2u * lane : (uint32_t)lane;
       for (int c = ow; c < nchunk; c += kGenOut, ++k) {
         const int cnt = min(64, g.n - 64 * c);
         const uint32_t first = base + wstep * (uint32_t)c;
         const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
         if (k % kGenNeedEvery == 0) LDS_ST(gen_need[ow][lane], first);
-        uint32_t spin = 0;
-        for (; seen <= last && spin < kGenSpinMax; ++spin) {  // wait for the recurrence
-          seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
-          if (seen <= last) __builtin_amdgcn_s_sleep(1);
-        }
-        if (spin == kGenSpinMax) {
-          gen_fail(g);
-          LDS_ST(gen_need[ow][lane], 0xffffffffu);
-          return;
+        if (seen <= last) {  // wait for the recurrence (the check of its bound only on this path)
+          uint32_t spin = 0;
+          for (; seen <= last && spin < kGenSpinMax; ++spin) {
+            seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
+            if (seen <= last) __builtin_amdgcn_s_sleep(1);
+          }
+          if (spin == kGenSpinMax) {
+            gen_fail(g);
+            LDS_ST(gen_need[ow][lane], 0xffffffffu);
+            return false;
+          }
         }
         GEN_FENCE();
         // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
@@ -1992,6 +1998,9 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
         const uint64_t bits = __builtin_amdgcn_ballot_w64(flag) & (cnt == 64 ? ~0ull : (1ull << cnt) - 1ull);
         if (lane < 2) *at(rec_out, (uint32_t)(2 * c * planes + p) + lane_planes) = (uint32_t)(lane ? bits >> 32 : bits);
       }
+      return true;
+      };
+      if (!(dbl ? chunks(std::true_type{}) : chunks(std::false_type{}))) return;
     }
     kpos += W;
   }

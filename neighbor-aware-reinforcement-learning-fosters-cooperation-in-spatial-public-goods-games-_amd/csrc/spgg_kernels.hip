@@ -1960,45 +1960,45 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       const uint32_t base = kpos + plane_word0((uint32_t)g.n, p);
       // (the chunk loop is instantiated per plane kind: the kind's branches leave the loop)
       auto chunks = [&](auto dbl_c) -> bool {
-      constexpr bool dbl = decltype(dbl_c)::value;
-      constexpr uint32_t wstep = dbl ? 128u : 64u;
-      const uint32_t wlane = dbl ? 2u * lane : (uint32_t)lane;
-      for (int c = ow; c < nchunk; c += kGenOut, ++k) {
-        const int cnt = min(64, g.n - 64 * c);
-        const uint32_t first = base + wstep * (uint32_t)c;
-        const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
-        if (k % kGenNeedEvery == 0) LDS_ST(gen_need[ow][lane], first);
-        if (seen <= last) {  // wait for the recurrence (the check of its bound only on this path)
-          uint32_t spin = 0;
-          for (; seen <= last && spin < kGenSpinMax; ++spin) {
-            seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
-            if (seen <= last) __builtin_amdgcn_s_sleep(1);
+        constexpr bool dbl = decltype(dbl_c)::value;
+        constexpr uint32_t wstep = dbl ? 128u : 64u;
+        const uint32_t wlane = dbl ? 2u * lane : (uint32_t)lane;
+        for (int c = ow; c < nchunk; c += kGenOut, ++k) {
+          const int cnt = min(64, g.n - 64 * c);
+          const uint32_t first = base + wstep * (uint32_t)c;
+          const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
+          if (k % kGenNeedEvery == 0) LDS_ST(gen_need[ow][lane], first);
+          if (seen <= last) {  // wait for the recurrence (the check of its bound only on this path)
+            uint32_t spin = 0;
+            for (; seen <= last && spin < kGenSpinMax; ++spin) {
+              seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
+              if (seen <= last) __builtin_amdgcn_s_sleep(1);
+            }
+            if (spin == kGenSpinMax) {
+              gen_fail(g);
+              LDS_ST(gen_need[ow][lane], 0xffffffffu);
+              return false;
+            }
           }
-          if (spin == kGenSpinMax) {
-            gen_fail(g);
-            LDS_ST(gen_need[ow][lane], 0xffffffffu);
-            return false;
+          GEN_FENCE();
+          // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
+          const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
+          const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
+          const uint32_t o = o0 + wlane;
+          const uint32_t x = rb[gen_spill(o)];
+          bool flag;
+          if (dbl) {
+            const uint32_t ah = mt_temper(x) >> 5;
+            flag = ah < th_hi;
+            if (ah == th_hi) flag = (mt_temper(rb[gen_spill(o + 1)]) >> 6) < th_lo;
+          } else {  // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
+            flag = (__builtin_popcount(x & kTemperBit0) & 1) != 0;
           }
+          // (lanes past n read stale words: masked)
+          const uint64_t bits = __builtin_amdgcn_ballot_w64(flag) & (cnt == 64 ? ~0ull : (1ull << cnt) - 1ull);
+          if (lane < 2) *at(rec_out, (uint32_t)(2 * c * planes + p) + lane_planes) = (uint32_t)(lane ? bits >> 32 : bits);
         }
-        GEN_FENCE();
-        // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
-        const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
-        const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
-        const uint32_t o = o0 + wlane;
-        const uint32_t x = rb[gen_spill(o)];
-        bool flag;
-        if (dbl) {
-          const uint32_t ah = mt_temper(x) >> 5;
-          flag = ah < th_hi;
-          if (ah == th_hi) flag = (mt_temper(rb[gen_spill(o + 1)]) >> 6) < th_lo;
-        } else {  // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
-          flag = (__builtin_popcount(x & kTemperBit0) & 1) != 0;
-        }
-        // (lanes past n read stale words: masked)
-        const uint64_t bits = __builtin_amdgcn_ballot_w64(flag) & (cnt == 64 ? ~0ull : (1ull << cnt) - 1ull);
-        if (lane < 2) *at(rec_out, (uint32_t)(2 * c * planes + p) + lane_planes) = (uint32_t)(lane ? bits >> 32 : bits);
-      }
-      return true;
+        return true;
       };
       if (!(dbl ? chunks(std::true_type{}) : chunks(std::false_type{}))) return;
     }

@@ -10,7 +10,8 @@ over every replica of the batch resident in HBM.  Default workload is cfg3 of
 BASELINE.json (L=200, r in {2.0..5.0} x kappa in {0,0.5,1.0} x 5 seeds = 105
 replicas, M=1, reputation state, w_P=1.0) — the L=200 single-GPU configuration
 the metric and its roofline target are quoted on.  Under torchrun each rank runs
-its own batch (seeds offset by rank: weak scaling); the only collective is the
+its own block of the config's seeds (cfg4: seeds 8k..8k+7 on rank k, so 8 ranks run
+BASELINE's seeds 0-63; weak scaling); the only collective is the
 final cooperation-rate gather (RCCL all_gather).
 
 value = executed agent-steps of all ranks / max-over-ranks wall time of the K
@@ -43,26 +44,41 @@ def runner_params(**kw):
 
 
 def workload(name, rank):
-    """(description, L, M2, state, [ReplicaParams]) for a BASELINE.json config."""
-    off = 1000 * rank
+    """(description, L, M2, state, [ReplicaParams]) of a BASELINE.json config for one rank.
+
+    Ranks split the config's seeds (BASELINE.json configs[3]/[4]: cfg4 = seeds 0-63, 8 per GPU;
+    cfg5 = seeds 0-7, one per GPU): rank k runs seeds k*S .. k*S+S-1, S = the config's seeds per
+    GPU, so N ranks together run seeds 0 .. N*S-1 -- the reference runner's replica set
+    (runner.py:136-154 fans the same replicas out over a process pool)."""
     if name == "cfg2":
+        off = rank
         return ("cfg2: L=200 r=3.0 kappa=1.0 M=1 reputation, 1 replica", 200, False, "reputation",
                 [runner_params(r=3.0, influence_factor=1.0, seed=off)])
-    if name == "cfg3":
+    if name == "cfg3":  # the r x kappa grid, 5 seeds per GPU
+        off = 5 * rank
         reps = [runner_params(r=2.0 + 0.5 * i, influence_factor=k, reward_weight_payoff=1.0, seed=off + s)
                 for i in range(7) for k in (0.0, 0.5, 1.0) for s in range(5)]
         return ("cfg3: L=200 r{2.0..5.0}x kappa{0,0.5,1}x5 seeds = 105 replicas, M=1 reputation, w_P=1.0",
                 200, False, "reputation", reps)
     if name == "cfg4":
+        off = 8 * rank
         return ("cfg4: L=200 r=3.0 kappa=1.0 M=2 action, 8 replicas per GPU", 200, True, "action",
                 [runner_params(r=3.0, influence_factor=1.0, seed=off + s) for s in range(8)])
     if name == "cfg5":
+        off = rank
         return ("cfg5: L=1000 r=3.6 kappa=1.0 M=1 reputation, 1 replica per GPU", 1000, False, "reputation",
                 [runner_params(r=3.6, influence_factor=1.0, seed=off)])
     if name == "run100":  # the shape one SPGG(...).run() of the reference's runner steps (runner.py:88-101)
+        off = rank
         return ("run100: L=100 r=3.0 kappa=1.0 M=1 reputation, 1 replica (one SPGG.run of the runner)", 100,
                 False, "reputation", [runner_params(r=3.0, influence_factor=1.0, seed=off)])
     raise SystemExit(f"unknown config {name}")
+
+
+def seed_range(reps):
+    """'a-b' (or 'a') of a rank's replica seeds, for the line's config."""
+    s = sorted({int(p.seed or 0) for p in reps})
+    return f"{s[0]}-{s[-1]}" if len(s) > 1 else f"{s[0]}"
 
 
 def latest_profile(name):
@@ -335,6 +351,7 @@ def main(argv=None):
         dist.all_gather(parts, buf)
         gathered_rows = np.stack([p_.cpu().numpy() for p_ in parts])
     value = agent_steps_all / wall_max
+    gathered_seed_max = max(int(p.seed or 0) for p in workload(args.config, world - 1)[4])
     per_step_dev_s = dev_ms / 1e3 / K
     step_agents = agent_steps / K
     achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
@@ -356,7 +373,8 @@ def main(argv=None):
             "data": "synthetic (reference init: S~Bernoulli(1/2), R=0, Q~U(-0.01,0.01))",
             "config": {"workload": desc, "window": f"iterations {W + 1}-{W + K}", "L": L, "replicas_per_gpu": len(reps),
                        "agents_per_gpu": n_agents, "second_order": M2, "state": state,
-                       "rng": args.rng, "streams_per_gpu": resident, "replica_groups": groups,
+                       "rng": args.rng, "seeds_rank0": seed_range(reps), "seeds_all_ranks": f"0-{int(gathered_seed_max)}",
+                       "streams_per_gpu": resident, "replica_groups": groups,
                        "cache_waves": waves, "mt_chains": mt_layout,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "gather": {"replicas": int(gathered_rows.shape[0] * gathered_rows.shape[1]),

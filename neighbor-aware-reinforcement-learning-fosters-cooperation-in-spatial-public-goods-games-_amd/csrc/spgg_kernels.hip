@@ -1896,7 +1896,8 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       lim = m > 0xffffffffu - (kGenNB - 1) * kMtBlock ? 0xffffffffu : m + (kGenNB - 1) * kMtBlock;        \
       if (F > lim) __builtin_amdgcn_s_sleep(2);                                                           \
     }                                                                                                     \
-    if (spin == kGenSpinMax) { /* this block is the last: rec_done publishes kGenDoneAbort */            \
+    if (F > lim) { /* the bound ran out (the condition, not the counter: a last poll that succeeds    \
+                      is no failure); this block is the last: rec_done publishes kGenDoneAbort */       \
       gen_fail(g);                                                                                        \
       aborted = true;                                                                                     \
       nblk = b + 1;                                                                                       \
@@ -1974,7 +1975,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
               seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
               if (seen <= last) __builtin_amdgcn_s_sleep(1);
             }
-            if (spin == kGenSpinMax) {
+            if (seen <= last) {  // (the condition itself: a last poll that succeeds is no failure)
               gen_fail(g);
               LDS_ST(gen_need[ow][lane], 0xffffffffu);
               return false;

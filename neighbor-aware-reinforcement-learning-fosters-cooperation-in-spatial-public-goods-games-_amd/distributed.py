@@ -66,11 +66,12 @@ def shard(items: Sequence, world: int, rank: int):
     return list(items[a:b])
 
 
-def gather_rows(local: np.ndarray, n_items: int, device=None, group=None) -> np.ndarray:
-    """All-gather each rank's (k_rank, m) float64 block back into (n_items, m), in replica order.
+def gather_rows(local: np.ndarray, n_items: int, device=None, group=None, dst: Optional[int] = None):
+    """Gather each rank's (k_rank, m) float64 block back into (n_items, m), in replica order.
 
-    Blocks are padded to the largest shard so a single fixed-size all_gather
-    suffices (no object pickling)."""
+    dst None: all_gather (every rank gets the rows); dst = a rank: gather to that rank only
+    (the others get None).  Blocks are padded to the largest shard so a single fixed-size
+    collective suffices (no object pickling)."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -86,8 +87,15 @@ def gather_rows(local: np.ndarray, n_items: int, device=None, group=None) -> np.
     buf = torch.zeros((rows, m), dtype=torch.float64, device=dev)
     if b > a:
         buf[: b - a] = torch.from_numpy(local).to(dev)
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
+    if dst is None:
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+    else:
+        root = dst if group is None else dist.get_global_rank(group, dst)
+        parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+        dist.gather(buf, parts, dst=root, group=group)
+        if rank != dst:
+            return None
     out = np.empty((n_items, m))
     for r in range(world):
         ra, rb_ = shard_range(n_items, world, r)
@@ -130,16 +138,25 @@ def coop_traces(engine) -> np.ndarray:
 
 
 def run_sharded(replicas, L: int, iterations: int, use_second_order=True,
-                state_representation="reputation", rng="mt19937", device=None, group=None):
-    """Run this rank's block of `replicas` on its GPU, then all-gather the summaries.
+                state_representation="reputation", rng="mt19937", device=None, group=None,
+                traces: str = "root"):
+    """Run this rank's block of `replicas` on its GPU, then gather the results.
 
     The rank's GPU is LOCAL_RANK (torchrun) unless `device` names one; replica k of
     the block keeps its global index (shard offset + k) as its Philox stream id, so a
     replica's stream -- and its trajectory in "philox" mode -- does not depend on the
-    world size.  Returns (summaries (N, 5) and cooperation-rate traces (N, iterations), both
-    on every rank, and this rank's BatchEngine) -- the one collective of the path."""
+    world size.  Returns (summaries, traces, engine):
+      summaries -- (N, 5) float64, SUMMARY_FIELDS, all-gathered to every rank;
+      traces    -- (N, iterations) cooperation-rate traces (coop_traces), gathered to rank 0
+                   only (traces="root", the default: ~8 B per replica and iteration, which
+                   the other ranks rarely need), to every rank ("all"), or not at all
+                   ("none"); None on a rank that does not receive them;
+      engine    -- this rank's BatchEngine (None for an empty shard).
+    These are the path's only collectives."""
     import torch.distributed as dist
     from . import engine as E
+    if traces not in ("root", "all", "none"):
+        raise ValueError(f"traces must be 'root', 'all' or 'none', not {traces!r}")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if device is None:
@@ -150,16 +167,19 @@ def run_sharded(replicas, L: int, iterations: int, use_second_order=True,
     mine = list(replicas[a:b])
     eng = None
     local = np.zeros((0, len(SUMMARY_FIELDS)))
-    traces = np.zeros((0, iterations))
+    tr = np.zeros((0, iterations))
     if mine:
         eng = E.BatchEngine(L, iterations, mine, use_second_order=use_second_order,
                             state_representation=state_representation, rng=rng, device=device,
                             replica_offset=a)
         eng.run(snapshots=False)
         local = replica_summaries(eng)
-        traces = coop_traces(eng)
+        tr = coop_traces(eng)
     if world == 1:
-        return local, traces, eng
+        return local, (None if traces == "none" else tr), eng
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else None
-    rows = gather_rows(np.concatenate([local, traces], axis=1), len(replicas), device=dev, group=group)
-    return rows[:, :len(SUMMARY_FIELDS)], rows[:, len(SUMMARY_FIELDS):], eng
+    summaries = gather_rows(local, len(replicas), device=dev, group=group)
+    out_tr = None
+    if traces != "none":
+        out_tr = gather_rows(tr, len(replicas), device=dev, group=group, dst=0 if traces == "root" else None)
+    return summaries, out_tr, eng

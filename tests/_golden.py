@@ -77,3 +77,49 @@ def assert_datasets_equal(got, want, exact=True, rtol=1e-5, atol=1e-8, skip=()):
             assert np.array_equal(g, w, equal_nan=w.dtype.kind == "f"), k
         else:
             np.testing.assert_allclose(g, w, rtol=rtol, atol=atol, equal_nan=True, err_msg=k)
+
+
+class DeepDigest:
+    """A deep run of the reference (tests/golden/make_deep_golden.py): sha256 digests of the
+    datasets compared bit for bit, every 10th value + the sums of the float histories."""
+
+    def __init__(self, name="deep_L100_10001"):
+        with open(os.path.join(GOLDEN_DIR, name + ".json")) as f:
+            d = json.load(f)
+        self.meta, self.exact, self.approx = d["meta"], d["exact"], d["approx"]
+        self.seed, self.kwargs = self.meta["seed"], self.meta["kwargs"]
+
+    @staticmethod
+    def digest(a):
+        import hashlib
+        a = np.ascontiguousarray(np.asarray(a))
+        return {"dtype": a.dtype.str, "shape": list(a.shape),
+                "sha256": hashlib.sha256(a.tobytes()).hexdigest()}
+
+    def check(self, datasets, q_table, R, Sn, ret, rtol=1e-5, atol=1e-9, mt_key=None):
+        """Assert a run's datasets and final state match: exact ones by digest (dtype, shape,
+        bytes), float histories at every 10th value and by their sums within rtol."""
+        finals_names = {"__q_table", "__R", "__Sn", "__ret", "__mt_key"}
+        want_names = set(self.exact) - finals_names | set(self.approx)
+        assert set(datasets) == want_names, sorted(set(datasets) ^ want_names)
+        finals = {"__q_table": q_table, "__R": R, "__Sn": np.asarray(Sn),
+                  "__ret": np.array([float(x) for x in ret])}
+        if mt_key is not None:
+            finals["__mt_key"] = np.asarray(mt_key, dtype=np.uint32)
+        for k, w in self.exact.items():
+            if k == "__mt_key" and mt_key is None:
+                continue
+            g = self.digest(finals[k] if k in finals else datasets[k])
+            assert g == w, (k, g["dtype"], g["shape"], w["dtype"], w["shape"])
+        for k, w in self.approx.items():
+            a = np.asarray(datasets[k], dtype=np.float64)
+            assert list(a.shape) == w["shape"], (k, a.shape, w["shape"])
+            flat = a.reshape(a.shape[0], -1) if a.ndim > 1 else a
+            vals = np.array([np.nan if v is None else v for v in
+                             (np.ravel(w["values"]) if flat.ndim == 1 else
+                              [x for row in w["values"] for x in row])], dtype=np.float64)
+            np.testing.assert_allclose(flat[::w["stride"]].reshape(-1), vals, rtol=rtol, atol=atol,
+                                       equal_nan=True, err_msg=k)
+            np.testing.assert_allclose(np.nansum(flat, axis=0), np.array(w["nansum"]), rtol=rtol,
+                                       atol=atol * flat.shape[0], err_msg=k + " (sum)")
+            assert int(np.isnan(flat).sum()) == w["nan_count"], k

@@ -106,3 +106,21 @@ def test_bench_world2_gloo():
     assert g["replicas"] == 2 and g["bytes"] == 2 * (1 + K) * 8
     want = np.mean([(100 * r + 3 + K) / (L * L) for r in range(world)])
     assert abs(g["mean_final_coop"] - want) < 1e-15
+
+
+def test_rank_seed_blocks_cover_baseline_configs():
+    """Ranks split the config's seeds (BASELINE.json configs[3]/[4]): 8 ranks of cfg4 run seeds
+    0-63, 8 per rank; 8 ranks of cfg5 run seeds 0-7; every rank keeps the same parameter grid."""
+    import bench
+    for name, per, total in (("cfg4", 8, 64), ("cfg5", 1, 8), ("cfg2", 1, 8), ("cfg3", 5, 40)):
+        seen = []
+        for rank in range(8):
+            desc, L, M2, state, reps = bench.workload(name, rank)
+            seeds = sorted({int(p.seed) for p in reps})
+            assert seeds == list(range(per * rank, per * rank + per)), (name, rank, seeds)
+            seen += seeds
+        assert sorted(seen) == list(range(total)), name
+    r0, r1 = bench.workload("cfg3", 0)[4], bench.workload("cfg3", 1)[4]
+    assert [(p.r, p.influence_factor) for p in r0] == [(p.r, p.influence_factor) for p in r1]
+    assert [p.seed for p in bench.workload("cfg4", 1)[4]] == list(range(8, 16))
+    assert bench.seed_range(bench.workload("cfg4", 7)[4]) == "56-63"

@@ -45,7 +45,8 @@ def _worker(rank, world, port, n, q):
         a, b = shard_range(n, world, rank)
         local = np.array([[i, i * 0.5, -i] for i in range(a, b)], dtype=np.float64).reshape(-1, 3)
         out = gather_rows(local, n)
-        q.put((rank, out))
+        root = gather_rows(local, n, dst=1)   # to rank 1 only
+        q.put((rank, out, root))
     finally:
         dist.destroy_process_group()
 
@@ -63,5 +64,9 @@ def test_gather_rows_world2_gloo(n):
         p.join(timeout=60)
         assert p.exitcode == 0
     want = np.array([[i, i * 0.5, -i] for i in range(n)], dtype=np.float64)
-    for _, out in res:
+    for rank, out, root in res:
         assert np.array_equal(out, want)
+        if rank == 1:
+            assert np.array_equal(root, want)
+        else:
+            assert root is None

@@ -674,3 +674,27 @@ def test_engines_in_sequence_reuse_library_streams(streams):
         eng.close()
         del flags
     assert seen[0] and seen[0] == seen[1] == seen[2]   # (the pool hands streams back last-in first-out)
+
+
+def test_dropin_deep_run_matches_reference_digest(tmp_path):
+    """SPGG(L=100, iterations=10001), the runner's shape (runner.py:88-101), through the
+    snapshot iterations 5000 and 10000 (spgg.py:153,397-402) against a digest of the reference's
+    own run (tests/golden/make_deep_golden.py): every dataset, Q / R / S, the return value, the
+    PNG set and the global MT19937 key the run leaves -- bit-exact; float histories 1e-5."""
+    from tests._golden import DeepDigest
+    d = DeepDigest()
+    orig = np.random.seed
+    np.random.seed = lambda s=None: orig(d.seed if s is None else s)
+    try:
+        m = spgg_amd.SPGG(**d.kwargs)
+    finally:
+        np.random.seed = orig
+    m.folder = str(tmp_path)
+    fn = str(tmp_path / "experiment_data.h5")
+    ret = m.run(fn)
+    got = read_datasets(fn)
+    st = np.random.get_state()
+    d.check(got, m.q_table, m.R, m._Sn, ret, mt_key=st[1], **FLOAT_TOL)
+    assert int(st[2]) == d.meta["mt_pos"]
+    assert m.algorithm.epsilon == d.meta["epsilon"]
+    assert sorted(os.listdir(tmp_path / "plots" / "snapshots")) == d.meta["png"]

@@ -93,6 +93,9 @@ def _worker(rank, world, ports, q):
         summ, traces, eng = D.run_sharded(reps, L=4, iterations=9, rng="philox")
         out["sharded"] = summ
         out["traces"] = traces
+        summ2, traces_all, _ = D.run_sharded(reps, L=4, iterations=9, rng="philox", traces="all")
+        out["traces_all"] = traces_all
+        out["sharded2"] = summ2
         out["engine"] = _FakeEngine.made[-1]
     finally:
         dist.destroy_process_group()
@@ -144,8 +147,15 @@ def test_launch_path_world2_gloo():
         assert e["device"] == o["rank"] and e["cur_dev"] == o["rank"]
         want = np.array([[s / 16, 1 - s / 16, s / 100, 0.0, 9.0] for s in range(5, 12)])
         np.testing.assert_allclose(o["sharded"], want)
-        # the cooperation-rate traces of every replica, gathered in replica order
-        np.testing.assert_allclose(o["traces"], [[(s + t) / 16 for t in range(1, 10)] for s in range(5, 12)])
+        # the cooperation-rate traces of every replica, gathered in replica order: to rank 0
+        # only by default, to every rank with traces="all"
+        want_tr = [[(s + t) / 16 for t in range(1, 10)] for s in range(5, 12)]
+        if o["rank"] == 0:
+            np.testing.assert_allclose(o["traces"], want_tr)
+        else:
+            assert o["traces"] is None
+        np.testing.assert_allclose(o["traces_all"], want_tr)
+        np.testing.assert_allclose(o["sharded2"], want)
 
     # sweep.main under torchrun env: each rank runs its block only, results complete
     cfg = SW.load_config(None)

@@ -48,7 +48,8 @@ using namespace spgg;
 //   1 = cheap hash instead of Philox, 2 = no history atomics, 4 = no ring recompute,
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
 //   16 = no workgroup totals (final barrier + epilogue), 512 = no per-agent Q / md / atd loads
-//   (synthetic values), 2048 = no per-agent Q / md / atd stores, 4096 = Q plane 0 read only (plane 1's
+//   (synthetic values), 2048 = no per-agent Q / md / atd stores, 8192 = no md loads / stores (the
+//   pending NI term reads +0), 4096 = Q plane 0 read only (plane 1's
 //   entries copied from it), 128 = memory only (the owned loads,
 //   staging and stores, no compute)
 #ifndef SPGG_ABLATE
@@ -176,7 +177,7 @@ namespace {
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_DR, off_DP, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_PP, off_DR, off_DP, bytes;
 };
 
 // Staged draw bits (MT19937 / inject, compile-time-width tiles): per region row, the draw-record
@@ -208,6 +209,7 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_D = off;    off += ((l.sw * l.sh + kPcPitch + 15) / 16) * 16;  // + slack: full-wave row reads
   l.off_A = off;    off += ((na + 15) / 16) * 16;
   l.off_PC = off;   off += (l.ah + 2) * kPcPitch;
+  l.off_PP = off;   off += (l.ah + 2) * kPcPitch;  // the same plane of S_{t-1} (recomputed NI record)
   off = (off + 15) / 16 * 16;
   l.off_DR = off;   off += draws ? l.ah * kDrawSlots * 2 * 4 : 0;
   l.off_DP = off;   off += draws ? l.ah * 2 * 2 * 4 : 0;
@@ -476,6 +478,38 @@ __device__ __forceinline__ void build_plus_counts_dw(uint8_t* pc, const uint8_t*
   }
 }
 
+// The plus-count plane of the PREVIOUS strategies S_{t-1}: bit 3 of every S_t byte (the
+// strategy its owner started iteration t-1 with), from the staged S window itself -- the
+// payoffs of iteration t-1 recomputed for the pending NI record (recomputed_record).
+__device__ __forceinline__ void build_plus_counts_prev(uint8_t* pc, const uint8_t* s, int sw, int rows) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int y = wave; y < rows; y += kWaves) {
+    const uint8_t* p = s + y * sw + lane;
+    const int cnt = ((p[1] >> 3) & 1) + ((p[sw] >> 3) & 1) + ((p[sw + 1] >> 3) & 1) + ((p[sw + 2] >> 3) & 1) +
+                    ((p[2 * sw + 1] >> 3) & 1);
+    pc[y * kPcPitch + lane] = (uint8_t)(cnt << 3);
+  }
+}
+template <int DWPR>
+__device__ __forceinline__ void build_plus_counts_prev_dw(uint8_t* pc, const uint8_t* splane, int sw, int rows,
+                                                          int soff) {
+  const uint32_t s0 = 8u * soff, s1 = s0 + 8u, s2 = s0 + 16u;
+  const int swd = sw >> 2;
+  constexpr uint32_t kB3 = 0x01010101u;
+  for (int task = threadIdx.x; task < rows * DWPR; task += kBlock) {
+    const int y = task / DWPR, xd = task - (task / DWPR) * DWPR;
+    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(splane) + y * swd + xd;
+    const uint32_t a0 = (r0[0] >> 3) & kB3, a1 = (r0[1] >> 3) & kB3;
+    const uint32_t b0 = (r0[swd] >> 3) & kB3, b1 = (r0[swd + 1] >> 3) & kB3;
+    const uint32_t c0 = (r0[2 * swd] >> 3) & kB3, c1 = (r0[2 * swd + 1] >> 3) & kB3;
+    const uint32_t cnt = __builtin_amdgcn_alignbit(a1, a0, s1) + __builtin_amdgcn_alignbit(b1, b0, s0) +
+                         __builtin_amdgcn_alignbit(b1, b0, s1) + __builtin_amdgcn_alignbit(b1, b0, s2) +
+                         __builtin_amdgcn_alignbit(c1, c0, s1);
+    *reinterpret_cast<uint32_t*>(pc + y * kPcPitch + xd * 4) = cnt << 3;
+  }
+}
+
 // Payoff of the region cell (ry, rx) (spgg.py:230-259, 373-377): the five
 // group defector counts are plus counts at the cell and its four axial
 // neighbours, each a byte offset into tb = the table of the cell's own
@@ -734,6 +768,48 @@ __device__ __forceinline__ float td_update(const TileArgs& a, const PT& pg, int 
   }
 }
 
+// The pending NI record of iteration t-1 RECOMPUTED in launch t (every operator but SARSA,
+// whose diagnostic select draws again, spgg.py:452): instead of storing max(0, max_diff) (f64)
+// and |alpha*td'| (f32) per agent in launch t-1 and loading them here (24 B per agent-step of a
+// kappa != 0 replica), launch t rebuilds the rewards of iteration t-1 over its region from the
+// S_t window's bit 3 (S_{t-1}: the payoffs) and bit 0 (a_{t-1}: the reputation reward), and
+// from them and the Q rows it holds (the table after the TD update of t-1, before its NI term)
+// the same two values, bit for bit (the same f64 operations on the same operands).
+template <bool M2>
+__device__ __forceinline__ double prev_max_diff(const double* rew, int ca, int w) {
+  // spgg.py:486-489 restated as phase 2 computes it: max over the 4 / 12 offsets of
+  // rew[nb] - rew[ca] (max is exact and order-free on non-NaN, never -0 rewards), then max(0, .)
+  const double r0 = rew[ca];
+  constexpr int KN = M2 ? 12 : 4;
+  const int nb[12] = {ca - w, ca + w, ca - 1, ca + 1, ca - 2 * w, ca + 2 * w, ca - 2, ca + 2,
+                      ca - w - 1, ca - w + 1, ca + w - 1, ca + w + 1};
+  double rw[KN];
+#pragma unroll
+  for (int k = 0; k < KN; ++k) rw[k] = rew[nb[k]];
+  double md = rw[0] - r0;
+#pragma unroll
+  for (int k = 1; k < KN; ++k) md = max_f64(md, rw[k] - r0);
+  return md > 0.0 ? md : 0.0;
+}
+
+// |diag_alpha * td'| of iteration t-1 (spgg.py:446-475) from the table after its TD update
+// (q, qb: before the NI term), its entry e = (s_old, a), its new state sn and reward rew --
+// what td_update returned in launch t-1.  eps_prev: eps of iteration t-1 (Expected SARSA).
+template <int ALG, typename PT>
+__device__ __forceinline__ float prev_diag_td(const double (&q)[4], const double (&qb)[ALG == ALG_DQ ? 4 : 1],
+                                              int e, int sn, double rew, const PT& pg, double eps_prev) {
+  if constexpr (ALG == ALG_DQ) {
+    return diag_td_dq(q, qb, e, sn, rew, pg);
+  } else {
+    double w0, w1, o0, o1;
+    select_row<0>(q, qb, sn, &w0, &w1);        // row s' of the updated table
+    select_row<0>(q, qb, e >> 1, &o0, &o1);    // row s_old: Q'[s, a] = q1
+    const double q1 = (e & 1) ? o1 : o0;
+    const double target2 = ALG == ALG_ES ? expected_q(w0, w1, eps_prev) : max_f64(w0, w1);
+    return (float)fabs(pg.diag_alpha * ((rew + pg.diag_gamma * target2) - q1));
+  }
+}
+
 // ONE launch = iteration t of every replica (or, fin_only, the final deferred
 // NI term).  TWC > 0: compile-time tile width, every tile full width (host:
 // L % TWC == 0), so LDS pitches and region divisions are immediates.
@@ -790,6 +866,8 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   constexpr int QB = ALG == ALG_DQ ? 1 : 0;
   constexpr int QW = QB ? 8 : 4;
   constexpr int PF = spgg_impl::pf_of(ALG);
+  // pending NI record recomputed from S_t's bits (prev_max_diff / prev_diag_td), not stored
+  constexpr bool RECOMP = ALG != ALG_SARSA;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -823,6 +901,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint8_t* sD = smem + ly.off_D;
   uint8_t* sA = smem + ly.off_A;
   uint8_t* sPC = smem + ly.off_PC;
+  uint8_t* sPP = smem + ly.off_PP;
   uint32_t* sDR = reinterpret_cast<uint32_t*>(smem + ly.off_DR);  // [row][slot][plane]
   uint2* sDP = reinterpret_cast<uint2*>(smem + ly.off_DP);         // [row][half] (plane 0, plane 1)
   // this replica's arrays: scalar bases, 32-bit element offsets (at())
@@ -936,12 +1015,12 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   // the pending NI record after every other load (its address waits for the replica's kappa): a
   // replica with kappa == 0 never uses it (phase 1a skips the NI term), so all its lanes read
   // the replica's first entry -- one cache line per wave instead of 12 B per agent
-  if (!(SPGG_ABLATE & 512)) {
+  if (!(SPGG_ABLATE & 512) && !RECOMP) {
     const bool ni_rec = __builtin_amdgcn_readfirstlane((int)(a.params[rep].kappa != 0.0)) != 0;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const uint32_t g = ni_rec ? agent_of(rc[u]) : 0u;
-      md_own[u] = *at(mdr, g);
+      md_own[u] = (SPGG_ABLATE & 8192) ? 0.0 : *at(mdr, g);  // 8192: md traffic floor probe
       atd_own[u] = (SPGG_ABLATE & 256) ? 0.f : *at(atdr, g);  // 256: atd traffic floor probe
     }
   }
@@ -996,6 +1075,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const double lam_den = uniform_f64(pending ? gmax_prev + pg.lambda_eps : 1.0);
   const double lam_rcp = uniform_f64(1.0 / lam_den);  // IEEE, once per workgroup
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
+  const double eps_prev = ALG == ALG_ES && pending ? a.eps[(size_t)rep * a.slots + t - 1] : 0.0;
   const uint64_t eps53 = uniform_u64(u53_threshold(eps_t));  // rand < eps_t as an integer compare
   // Philox key: 64-bit seed folded with the global replica id (distinct streams per replica)
   const uint32_t pkey = (uint32_t)pg.seed ^ (uint32_t)(pg.seed >> 32) * 0x85EBCA6Bu ^
@@ -1040,8 +1120,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
       store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u]);
-      *at(mdr, agent_of(rc[u])) = md_own[u];
-      *at(atdr, agent_of(rc[u])) = atd_own[u];
+      if (!RECOMP) {
+        *at(mdr, agent_of(rc[u])) = md_own[u];
+        *at(atdr, agent_of(rc[u])) = atd_own[u];
+      }
       *at(Sout, agent_of(rc[u])) = sSv[(r + HS) * ly.sw + (c + HS)];
       if (!AS) *at(Rout, agent_of(rc[u])) = sRv[(r + HA) * ly.aw + (c + HA)];
     }
@@ -1051,6 +1133,30 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (!fin_only) {
     if constexpr (TWC > 0) build_plus_counts_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPC, sD, ly.sw, ah + 2, soffS);
     else build_plus_counts(sPC, sDv, ly.sw, ah + 2);
+  }
+  // the rewards of iteration t-1 over the region (tile + ring), into sRew (phase 1a reads them;
+  // phases 1b / 1c overwrite them with iteration t's after the barrier that ends phase 1a)
+  const bool rec_prev = RECOMP && pending && kappa != 0.0;  // workgroup-uniform
+  if (rec_prev) {
+    if constexpr (TWC > 0) build_plus_counts_prev_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPP, sS, ly.sw, ah + 2, soffS);
+    else build_plus_counts_prev(sPP, sSv, ly.sw, ah + 2);
+    __syncthreads();  // both plus-count planes
+    const int dr = kBlock / aw, dc = kBlock - (kBlock / aw) * aw;
+    int ry = tid / aw, rx = tid - (tid / aw) * aw;
+    for (int k = tid; k < aw * ah; k += kBlock) {
+      const uint8_t b = sSv[(ry + (HS - HA)) * ly.sw + (rx + (HS - HA))];
+      const double P = payoff_pc(sPP, ry, rx, tab + (((b >> 3) & 1) ? 6 : 0), hp.norm_min, hp.norm_den, hp.norm_rcp);
+      const double rr = (b & 1) ? 0.0 : 0.5;                    // a_{t-1} = S_t (spgg.py:424-427)
+      const double wpp = w_p * P, wrr = w_rep * rr;
+      sRew[ry * ly.aw + rx] = wpp + wrr;
+      ry += dr;
+      rx += dc;
+      if (rx >= aw) {
+        rx -= aw;
+        ++ry;
+      }
+    }
+    __syncthreads();  // rewards of iteration t-1
   }
   // draw bits repacked to the region (DSTAGE): word (row ry, half h) holds cells rx = 32h ..
   // 32h+31 -- bit offA + rx of the row's first three groups for rx < a_len, bit offB + rx -
@@ -1107,8 +1213,17 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         // U(-0.01,0.01) draws and TD sums of finite values give +0 for exact zeros),
         // and the NI percent is exactly 0
         if (kappa != 0.0) {
-          const double mdp = md_own[u];
-          const float atdv = atd_own[u];
+          double mdp;
+          float atdv;
+          if constexpr (RECOMP) {  // the record of t-1 from its rewards and the held table
+            const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
+            const int ca = (r + HA) * ly.aw + (c + HA);
+            mdp = prev_max_diff<M2>(sRew, ca, ly.aw);
+            atdv = prev_diag_td<ALG>(q[u], qb[u], e, (b >> 4) & 1, sRew[ca], hp, eps_prev);
+          } else {
+            mdp = md_own[u];
+            atdv = atd_own[u];
+          }
           const double nu = pending_nu(b, mdp, kappa, lam_den, lam_rcp);
           // Q[s,a] += nu as exact masked FMAs: fma(1, nu, x) = x + nu, fma(0, nu, x) = x
 #pragma unroll
@@ -1293,7 +1408,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     // the stored diagnostic |alpha*td'| (kappa == 0: the NI percent it feeds is exactly 0), as a
     // scalar flag (an f64 compare has no scalar form and was repeated on the VALU per agent)
     const bool ni_on = __builtin_amdgcn_readfirstlane((int)(kappa != 0.0)) != 0;
-    const bool diag_on = ni_on;
+    const bool diag_on = ni_on && !RECOMP;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
       const int r = rc[u] >> 16, c = (rc[u] >> 8) & 0xff;
@@ -1342,7 +1457,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       bmax = max_f64(bmax, mdp);
       // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
       // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)
-      if (ni_on && !(SPGG_ABLATE & 2048)) *at(mdr, agent_of(rc[u])) = mdp;
+      if (ni_on && !RECOMP && !(SPGG_ABLATE & (2048 | 8192))) *at(mdr, agent_of(rc[u])) = mdp;
       *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
       *at(Rout, agent_of(rc[u])) = sRn[ca];
       const int bslot = (int)(int16_t)(uint16_t)(bsw >> (16 * u));  // (table: border_slot_table)

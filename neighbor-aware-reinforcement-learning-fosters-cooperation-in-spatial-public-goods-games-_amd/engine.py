@@ -314,12 +314,14 @@ class BatchEngine:
         self._flushed = False
 
     def state_bytes_per_replica(self) -> int:
-        """Bytes of per-agent state one iteration reads and writes (Q, md, atd, the
-        S / R ping-pong, ~10 % border records): the Infinity-Cache working set.
-        Budget SPGG_CACHE_MB (default 240 of the MI355X's 256 MB: measured knee for
-        L=200 between 227 and 272 MB, profiles/r01/current/replicas_sweep_*)."""
+        """Bytes of per-agent state one iteration reads and writes (Q, the S / R ping-pong,
+        ~10 % border records; SARSA also the stored pending NI record md + atd, which the
+        other operators recompute): the Infinity-Cache working set.  Budget SPGG_CACHE_MB
+        (default 240 of the MI355X's 256 MB: measured knee for L=200 between 227 and 272 MB,
+        profiles/r01/current/replicas_sweep_*)."""
         rsz = 1 if all(p.rep_unit() is not None for p in self.reps) else 8
-        return int(self.n * (self.QW * 8 + 8 + 4 + 2 + 2 * rsz) * 1.1)
+        rec = 8 + 4 if self.alg == C.ALG_SARSA else 0
+        return int(self.n * (self.QW * 8 + rec + 2 + 2 * rsz) * 1.1)
 
     # -- setup ---------------------------------------------------------------
     def _alloc(self):
@@ -621,9 +623,12 @@ class BatchEngine:
         """Execute iterations until `iterations` or every replica is absorbed.
 
         Turns of `chunk` iterations.  The absorbing-stop check of a turn is an asynchronous
-        copy of the stop flags; the host reads it one turn later (the device never idles at
-        a turn boundary; absorbed replicas' launches return at once, so running on past an
-        absorbing stop changes no result).  Snapshot iterations sync."""
+        copy of the stop flags; the host reads it one turn later, so the device never idles
+        at a turn boundary.  The price of the lag: once every replica has absorbed, one more
+        turn is already enqueued (up to `chunk` step launches that return after their loads,
+        plus MT19937 generator chunks), and a group is retired one turn late.  Absorbed
+        replicas' launches change nothing, so results are unaffected; only the wall time of a
+        run that absorbs early carries that turn.  Snapshot iterations sync."""
         stops = set()
         if snapshots:
             stops |= {i for i in SNAPSHOT_ITERS if i <= self.T}

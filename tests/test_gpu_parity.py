@@ -321,20 +321,23 @@ def test_philox_mode_deterministic_and_sane():
         assert h["epsilon_history_final"][0] == max(0.5 * 0.99, 0.01)
 
 
-@pytest.mark.parametrize("kappa,M2", [(1.0, False), (0.0, False), (1.0, True)])
-def test_philox_statistical_parity(kappa, M2):
+@pytest.mark.parametrize("kappa,M2,state", [(1.0, False, "reputation"), (0.0, False, "reputation"),
+                                            (1.0, True, "reputation"), (1.0, True, "action")])
+def test_philox_statistical_parity(kappa, M2, state):
     """The bench's Philox stream against the reference's MT19937 stream at the
     bench's lattice size (L=200): ensembles of 12 replicas per stream, same init
     law, must agree in the mean cooperation rate, the mean switch counts and the
     mean NI share at every checkpoint within 5 standard errors of the difference
-    (+ 2e-3 absolute for near-deterministic phases).  Statistical parity is what
-    the bench's number rests on."""
-    L, T, n = 200, 200, 12
+    (+ 2e-3 absolute for near-deterministic phases).  700 iterations: eps reaches
+    eps_min at ~390, so the checkpoints cover the steady state the headline and the
+    whole runs spend > 96 % of their time in; M=2 action state is cfg4's shape.
+    Statistical parity is what the bench's number rests on."""
+    L, T, n = 200, 700, 12
     runs = {}
     for rng, base in (("mt19937", 0), ("philox", 1000)):
         reps = [_runner_params(seed=base + s, influence_factor=kappa, r=3.6, reward_weight_payoff=1.0)
                 for s in range(n)]
-        eng = BatchEngine(L, T, reps, use_second_order=M2, rng=rng)
+        eng = BatchEngine(L, T, reps, use_second_order=M2, state_representation=state, rng=rng)
         eng.run(snapshots=False)
         hs = eng.histories()
         eng.close()
@@ -346,7 +349,7 @@ def test_philox_statistical_parity(kappa, M2):
             return np.concatenate([x, np.full(T - 1 - len(x), fill)])
         a = np.stack([pad(h[key]) for h in runs["mt19937"]])
         b = np.stack([pad(h[key]) for h in runs["philox"]])
-        for t in (0, 9, 49, 99, T - 2):
+        for t in (0, 9, 49, 99, 199, 399, 449, 549, T - 2):
             se = np.sqrt(a[:, t].var(ddof=1) / n + b[:, t].var(ddof=1) / n)
             tol = 5 * se + 2e-3 * max(1.0, abs(a[:, t].mean()))
             assert abs(a[:, t].mean() - b[:, t].mean()) <= tol, (key, t, a[:, t].mean(), b[:, t].mean(), se)
@@ -435,7 +438,8 @@ def test_cache_blocked_waves_match_concurrent_groups(rng, monkeypatch):
     res = {}
     for mode in ("resident", "waves"):
         if mode == "waves":
-            monkeypatch.setenv("SPGG_CACHE_MB", "0.2")   # 10 x ~48 KB of state: 3 waves
+            # 10 x ~36 KB of state (Q-learning recomputes its pending NI record: no md / atd): 3 waves
+            monkeypatch.setenv("SPGG_CACHE_MB", "0.15")
             monkeypatch.setenv("SPGG_CHUNK", "7")
         eng = BatchEngine(L, T, reps, use_second_order=True, rng=rng, streams=6)
         if mode == "waves":

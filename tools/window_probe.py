@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--preheat", type=int, default=0)
     ap.add_argument("--streams", type=int, default=None)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--clock", type=int, default=0,
+                    help="us of a clock probe (build_ablate/libclockprobe.so, tools/clock_probe.hip) run on "
+                         "its own stream beside each window: the chip's effective clock in that window")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -50,25 +53,40 @@ def main():
     torch.cuda.synchronize()
     cur = torch.cuda.current_stream()
     evs = []
+    clk = None
+    if a.clock:
+        import ctypes
+        clib = ctypes.CDLL(os.path.join(ROOT, "build_ablate", "libclockprobe.so"))
+        nwin = -(-a.upto // a.win)
+        clk = torch.zeros(2 * nwin, dtype=torch.int64, device="cuda")
+        cstream = torch.cuda.Stream()
     t = a.first
     while t < a.upto + a.first:
         k = min(a.win, a.upto + a.first - t)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(cur)
+        if clk is not None:
+            cstream.wait_event(e0)
+            assert clib.clock_probe_launch(ctypes.c_void_p(clk.data_ptr()), len(evs), a.clock,
+                                           ctypes.c_void_p(cstream.cuda_stream)) == 0
         eng.step(k)
         e1.record(cur)
         torch.cuda.synchronize()   # one window in flight at a time (as the bench's timed region)
+        if clk is not None:
+            torch.cuda.synchronize()
         evs.append((t + 1, k, e0.elapsed_time(e1)))
         t += k
     st = eng.stats_folded().cpu().numpy()
     n = L * L
     print(f"{desc} ({a.rng}, groups {eng.G}, streams {eng.resident}, apt/tile {eng.tile})", flush=True)
-    print("window      us/iter   eps     switches/agent  coop", flush=True)
-    for t0, k, ms in evs:
+    clocks = clk.view(-1, 2).cpu().numpy() if clk is not None else None
+    print("window      us/iter   eps     switches/agent  coop" + ("    MHz" if clk is not None else ""), flush=True)
+    for w, (t0, k, ms) in enumerate(evs):
         sl = slice(t0, t0 + k)
         sw = (st[:, sl, C.ST_SW_CD].sum() * 2 + 0.0) / (len(reps) * k * n)
         coop = st[:, sl, C.ST_NCOOP].mean() / n
-        print(f"{t0:4d}-{t0 + k - 1:<5d} {ms * 1e3 / k:8.2f}  {eng.eps_host[0, t0]:.4f}  {sw:10.4f}  {coop:8.4f}",
+        mhz = f"  {clocks[w, 0] / max(clocks[w, 1], 1) * 100:7.0f}" if clocks is not None else ""
+        print(f"{t0:4d}-{t0 + k - 1:<5d} {ms * 1e3 / k:8.2f}  {eng.eps_host[0, t0]:.4f}  {sw:10.4f}  {coop:8.4f}{mhz}",
               flush=True)
     eng.close()
 

@@ -2,8 +2,9 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3] [--rng philox]
 
-Default window: iterations 401-600 (eps at eps_min: the steady state of a run); the line also
-carries the whole 10,000-iteration run (full_run) and the MT19937 product path (mt19937).
+Default window: the driver's, iterations 6-25 (--warmup 5 --steps 20); the line also carries
+the steady window 401-600 (eps at eps_min), the whole 10,000-iteration run (full_run) and the
+MT19937 product path (mt19937).
 
 A "step" is one iteration of the reference's run loop (src/model/spgg.py:368-592)
 over every replica of the batch resident in HBM.  Default workload is cfg3 of
@@ -234,11 +235,13 @@ def full_run(L, M2, state, reps, rng, streams, T, offset, turn=256):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    # untimed iterations before the window: by 400, eps has decayed to eps_min (0.5 * 0.99^t
-    # reaches 0.01 at t = 390) -- the steady state a 10,000-iteration run spends >96 % of its
-    # iterations in ("Long configs": time a steady window after eps reaches eps_min)
-    ap.add_argument("--warmup", type=int, default=400)
+    # the driver's own window (bench.py --steps 20 --warmup 5: iterations 6-25, eps 0.48 -> 0.40,
+    # right after the engine is made); the line also carries the steady window 401-600 (eps at
+    # eps_min from t = 390: what a 10,000-iteration run spends >96 % of its iterations in) and the
+    # whole run
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-steady", action="store_true", help="skip the steady window (iterations 401-600)")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--rng", default="philox", choices=["philox", "mt19937"])
     ap.add_argument("--streams", type=int, default=None,
@@ -288,7 +291,7 @@ def main(argv=None):
         desc += f" [experiment: {args.replicas} replicas]"
     K, W = args.steps, args.warmup
 
-    def window(rng):
+    def window(rng, W=W, K=K):
         """W untimed + K timed iterations of a fresh engine in `rng` mode (barrier +
         synchronize on both sides; max over ranks): the executed agent-steps, times, layout."""
         eng = E.BatchEngine(L, K + W, reps, use_second_order=M2, state_representation=state, rng=rng,
@@ -359,9 +362,15 @@ def main(argv=None):
     resident, groups, waves = main_w["resident"], main_w["groups"], main_w["waves"]
     # the drop-in SPGG.run / sweep path: the device MT19937 stream, bit-identical to the reference
     mt_w = window("mt19937") if args.rng == "philox" and not args.no_mt else None
+    steady = None
+    if not args.no_steady and (W, K) != (400, 200):
+        steady = window(args.rng, 400, 200)
 
     traffic = None
-    tfile = latest_profile(f"traffic_{args.config}.json")
+    # the traffic measured in this very window (profiles/r<NN>/traffic_<config>_w<a>-<b>.json), else
+    # the config's generic file (a different window: named in traffic_unit)
+    tfile = latest_profile(f"traffic_{args.config}_w{W + 1}-{W + K}.json") or latest_profile(
+        f"traffic_{args.config}.json")
     if tfile and args.rng == "philox":
         # measured HBM bytes per agent-step (rocprofv3 PMC passes of this same command)
         traffic = json.load(open(tfile))["bytes_per_agent_step"] * step_agents
@@ -401,6 +410,15 @@ def main(argv=None):
         T_full = FULL_RUN_ITERS.get(args.config, 0) if args.full_run < 0 else args.full_run
         if args.full_run < 0 and wall_max / K * T_full > 60.0:
             T_full = 0
+        if steady:
+            sd = steady["dev_ms"] / 1e3 / 200
+            line["steady_window"] = {
+                "window": "iterations 401-600", "value": steady["agent_steps_all"] / steady["wall_max"],
+                "unit": "agent-steps/s", "ms_per_step": steady["wall_max"] * 1e3 / 200,
+                "device_ms_per_step": sd * 1e3,
+                "roofline_frac": ALGO_BYTES_PER_AGENT_STEP * steady["agent_steps"] / 200 / sd / 1e9 / HBM_PEAK_GBS,
+                "note": "the same workload after eps reached eps_min (t >= 390): the regime a 10,000-iteration "
+                        "run spends >96 % of its iterations in; a fresh engine, 400 untimed iterations"}
         if mt_w:
             line["mt19937"] = {
                 "value": mt_w["agent_steps_all"] / mt_w["wall_max"], "unit": "agent-steps/s",

@@ -74,7 +74,7 @@ def _worker(rank, world, port, q):
                       LOCAL_RANK=str(rank), SPGG_DIST_BACKEND="gloo")
     out = io.StringIO()
     with contextlib.redirect_stdout(out):
-        bench.main(["--config", "cfg2", "--steps", "5", "--warmup", "3", "--no-cpu-baseline", "--no-mt",
+        bench.main(["--config", "cfg2", "--steps", "5", "--warmup", "3", "--no-cpu-baseline", "--no-mt", "--no-steady",
                     "--full-run", "0"])
     q.put(dict(rank=rank, stdout=out.getvalue(), dev=cur["dev"], made=FakeEngine.made))
 

@@ -177,7 +177,7 @@ namespace {
 
 struct LdsLayout {
   int sw, sh, aw, ah;
-  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_PP, off_DR, off_DP, bytes;
+  int off_Rew, off_R, off_Rn, off_S, off_D, off_A, off_PC, off_DR, off_DP, bytes;
 };
 
 // Staged draw bits (MT19937 / inject, compile-time-width tiles): per region row, the draw-record
@@ -209,7 +209,6 @@ __host__ __device__ inline LdsLayout lds_layout(int tw, int th, int HS, int HA, 
   l.off_D = off;    off += ((l.sw * l.sh + kPcPitch + 15) / 16) * 16;  // + slack: full-wave row reads
   l.off_A = off;    off += ((na + 15) / 16) * 16;
   l.off_PC = off;   off += (l.ah + 2) * kPcPitch;
-  l.off_PP = off;   off += (l.ah + 2) * kPcPitch;  // the same plane of S_{t-1} (recomputed NI record)
   off = (off + 15) / 16 * 16;
   l.off_DR = off;   off += draws ? l.ah * kDrawSlots * 2 * 4 : 0;
   l.off_DP = off;   off += draws ? l.ah * 2 * 2 * 4 : 0;
@@ -866,8 +865,12 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   constexpr int QB = ALG == ALG_DQ ? 1 : 0;
   constexpr int QW = QB ? 8 : 4;
   constexpr int PF = spgg_impl::pf_of(ALG);
-  // pending NI record recomputed from S_t's bits (prev_max_diff / prev_diag_td), not stored
-  constexpr bool RECOMP = ALG != ALG_SARSA;
+  // pending NI record recomputed from S_t's bits (prev_max_diff / prev_diag_td), not stored: in
+  // the large-batch kernels (the operator's most agents per thread), where the 24 B per agent-step
+  // it saves bound the launch (cfg3 65.5 -> 64.1 us/step in the driver's window, 54.2 -> 53.2
+  // steady); the latency-bound small batches (two / one agent per thread) keep the stored record,
+  // where the region pass's VALU sits on the critical path (cfg4 steady 12.2 -> 14.9 us/step)
+  constexpr bool RECOMP = ALG != ALG_SARSA && APT == spgg_impl::apt_of(ALG);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -901,7 +904,11 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint8_t* sD = smem + ly.off_D;
   uint8_t* sA = smem + ly.off_A;
   uint8_t* sPC = smem + ly.off_PC;
-  uint8_t* sPP = smem + ly.off_PP;
+  // the plus-count plane of S_{t-1} (recomputed NI record) shares the ring records' space past
+  // ly.bytes: it is dead before phase 1a writes the records (the host sizes the larger of the two;
+  // a plane of its own took the step workgroup's LDS past the room a generator workgroup needs
+  // beside five of them: cfg3 MT19937 whole run 71.4-72.2 -> 70.5-71.2 us/iter)
+  uint8_t* sPP = smem + ly.bytes;
   uint32_t* sDR = reinterpret_cast<uint32_t*>(smem + ly.off_DR);  // [row][slot][plane]
   uint2* sDP = reinterpret_cast<uint2*>(smem + ly.off_DP);         // [row][half] (plane 0, plane 1)
   // this replica's arrays: scalar bases, 32-bit element offsets (at())
@@ -2304,12 +2311,19 @@ constexpr long long kTwoPerThreadTiles = 800;
 // MT19937 generator layout (spgg_mt_chains).  One chain generates a replica's draws at
 // ~200 ns per 227 words (measured: 119-215 ns with the steps running), i.e. ~W/227*0.2 us
 // per iteration of W words; the steps take ~15 ps per agent of the batch (cfg3: 62 us for
-// 4.2e6 agents), >= ~8 us.  Chains per replica: a power of two with 4x the needed rate; a
+// 4.2e6 agents), >= ~8 us.  Chains per replica: a power of two with kGenRateMargin x the needed rate; a
 // chain covers >= ~1e6 words (a jump costs ~20 us on 8 workgroups) and a chunk >= 128
 // iterations (cfg3, 105 x L=200, us/step by chains x iterations per chain: 16x4 86.0,
 // 32x2 96.4 -- 64-iteration chunks; 16x9 71.2, 8x18 72.7, 32x4 74.0, 64x2 74.8 -- 128-144;
 // profiles/r03/mt_chain_layouts.txt); the draw ring (2 chunks) stays <= 512 MB.  Lattices
 // under 4096 words per iteration keep one chain.
+// Chains generate at kGenRateMargin x the rate the steps consume: each generator workgroup beyond
+// the one a CU holds beside five step workgroups displaces a step workgroup for its whole chunk,
+// so more chains cost more than they hide (cfg3 MT19937 whole run, 3000 iterations, per-process:
+// 2 chains 69.4 us/iter -- too slow to keep up -- 4 chains 65.6-66.0, 8 (round 4's 4x) 69.5-70.1,
+// 16 72.3; profiles/r05/mt_chains_cfg3.txt).
+constexpr double kGenRateMargin = 2.0;
+
 void choose_mt_chains(spgg_ctx* c) {
   const spgg_config& cfg = c->cfg;
   const long long W = draw_mt_words(c->n, draw_planes(cfg.algorithm));
@@ -2318,7 +2332,7 @@ void choose_mt_chains(spgg_ctx* c) {
   if (W >= 4096) {
     const double gen_ns = W / 227.0 * 200.0;
     const double step_ns = std::max(8000.0, (double)batch * c->n * 0.015);
-    const double need = 4.0 * gen_ns / step_ns;
+    const double need = kGenRateMargin * gen_ns / step_ns;
     while (chains < 256 && chains < need) chains *= 2;
     if (chains > 1)
       per = (int)std::max((1000000 + W - 1) / W, (long long)((128 + chains - 1) / chains));
@@ -2747,8 +2761,9 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   }
   int rc = hip_check(c, hipSetDevice(cfg->device), "hipSetDevice");
   if (!rc) rc = build_ring_table(c);
-  if (!rc) {  // + the ring cells' border records
-    c->lds_bytes += (size_t)c->ring_max * spgg_impl::pf_of(cfg->algorithm) * sizeof(double);
+  if (!rc) {  // + the ring cells' border records (or the S_{t-1} plus-count plane that shares them)
+    c->lds_bytes += std::max((size_t)c->ring_max * spgg_impl::pf_of(cfg->algorithm) * sizeof(double),
+                             (size_t)(ly.ah + 2) * kPcPitch);
     if (c->lds_bytes > 160 * 1024) rc = fail(c, SPGG_E_ARG, "tile LDS footprint exceeds 160 KB");
   }
   if (rc) {

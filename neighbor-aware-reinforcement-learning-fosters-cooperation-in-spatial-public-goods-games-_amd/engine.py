@@ -316,7 +316,8 @@ class BatchEngine:
     def state_bytes_per_replica(self) -> int:
         """Bytes of per-agent state one iteration reads and writes (Q, the S / R ping-pong,
         ~10 % border records; SARSA also the stored pending NI record md + atd, which the
-        other operators recompute): the Infinity-Cache working set.  Budget SPGG_CACHE_MB
+        other operators' large-batch kernels recompute -- the batches this budget can split):
+        the Infinity-Cache working set.  Budget SPGG_CACHE_MB
         (default 240 of the MI355X's 256 MB: measured knee for L=200 between 227 and 272 MB,
         profiles/r01/current/replicas_sweep_*)."""
         rsz = 1 if all(p.rep_unit() is not None for p in self.reps) else 8

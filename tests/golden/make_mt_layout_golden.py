@@ -7,8 +7,8 @@ chains x iterations-per-chain iterations and every chunk boundary re-jumps the c
 These cases run past at least one boundary of the layout `choose_mt_chains` picks for
 them (asserted by tests/test_gpu_mt_layouts.py through spgg_mt_chains):
 
-  run100  L=100, runner constants, T=1200          layout 16 x 34 (544-iteration chunks)
-  cfg3    the 105-replica bench batch, T=300        layout  8 x 16 (128), 4 replicas checked
+  run100  L=100, runner constants, T=1200          layout  8 x 34 (272-iteration chunks)
+  cfg3    the 105-replica bench batch, T=300        layout  4 x 32 (128), 4 replicas checked
   cfg5    L=1000, r=3.6, T=260                      layout 256 x 1 (256)
 
 Recorded per replica, from oracle/spgg_oracle.py (itself pinned bit-exactly to the
@@ -46,11 +46,11 @@ def digest(a, dtype):
 
 
 def cases():
-    out = {"run100": dict(L=100, T=1200, M2=False, state="reputation", layout=[16, 34],
+    out = {"run100": dict(L=100, T=1200, M2=False, state="reputation", layout=[8, 34],
                           replicas=[dict(RUNNER, seed=0)], checked=[0])}
     cfg3 = [dict(RUNNER, r=2.0 + 0.5 * i, influence_factor=k, reward_weight_payoff=1.0, seed=s)
             for i in range(7) for k in (0.0, 0.5, 1.0) for s in range(5)]
-    out["cfg3"] = dict(L=200, T=300, M2=False, state="reputation", layout=[8, 16], replicas=cfg3,
+    out["cfg3"] = dict(L=200, T=300, M2=False, state="reputation", layout=[4, 32], replicas=cfg3,
                        checked=list(CFG3_CHECKED))
     out["cfg5"] = dict(L=1000, T=260, M2=False, state="reputation", layout=[256, 1],
                        replicas=[dict(RUNNER, r=3.6, seed=0)], checked=[0])

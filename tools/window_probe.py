@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--preheat", type=int, default=0)
     ap.add_argument("--streams", type=int, default=None)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--hot-ms", type=float, default=0.0,
+                    help="after making the measured engine, keep the GPU streaming memory for this many "
+                         "ms (torch copies of a 1 GiB buffer) right before the first window")
     ap.add_argument("--clock", type=int, default=0,
                     help="us of a clock probe (build_ablate/libclockprobe.so, tools/clock_probe.hip) run on "
                          "its own stream beside each window: the chip's effective clock in that window")
@@ -48,6 +51,16 @@ def main():
         e0.close()
     eng = BatchEngine(L, a.upto + a.first, reps, use_second_order=M2, state_representation=state, rng=a.rng,
                       streams=a.streams, lib_path=a.lib)
+    if a.hot_ms > 0:
+        buf = torch.empty(2 ** 27, dtype=torch.float64, device="cuda")
+        dst = torch.empty_like(buf)
+        torch.cuda.synchronize()
+        t_end = time.perf_counter() + a.hot_ms / 1e3
+        while time.perf_counter() < t_end:
+            for _ in range(4):
+                dst.copy_(buf)
+            torch.cuda.synchronize()
+        del buf, dst
     if a.first:
         eng.step(a.first)
     torch.cuda.synchronize()

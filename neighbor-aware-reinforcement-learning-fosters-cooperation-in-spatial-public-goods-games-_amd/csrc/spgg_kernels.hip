@@ -788,7 +788,7 @@ __device__ __forceinline__ double prev_max_diff(const double* rew, int ca, int w
   double md = rw[0] - r0;
 #pragma unroll
   for (int k = 1; k < KN; ++k) md = max_f64(md, rw[k] - r0);
-  return md > 0.0 ? md : 0.0;
+  return max_f64(md, 0.0);  // max(0, md): one v_max_f64 (md is never -0)
 }
 
 // |diag_alpha * td'| of iteration t-1 (spgg.py:446-475) from the table after its TD update
@@ -1460,7 +1460,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         if constexpr (M2) ks = better ? kk : ks;
       }
       const int dp = abest == act ? 1 : 0;
-      const double mdp = md > 0.0 ? md : 0.0;
+      const double mdp = max_f64(md, 0.0);  // max(0, md), one op (md is never -0: rewards are never -0)
       bmax = max_f64(bmax, mdp);
       // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
       // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)

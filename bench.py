@@ -304,17 +304,24 @@ def main(argv=None):
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
-        stream = torch.cuda.current_stream()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # HIP events on the streams the step kernels run on (every replica group's), first start
+        # to last end; the device is synchronised on both sides, so the groups' streams need no
+        # ordering against the current stream (eng.step(ordered=False): two cross-stream waits
+        # cost a 20-iteration window ~130 us, tools/window_timeline.py)
+        streams = eng.launch_streams()
+        ev0 = [torch.cuda.Event(enable_timing=True) for _ in streams]
+        ev1 = [torch.cuda.Event(enable_timing=True) for _ in streams]
         t0 = time.perf_counter()
-        ev0.record(stream)
-        eng.step(K)
-        ev1.record(stream)
+        for e, s_ in zip(ev0, streams):
+            e.record(s_)
+        eng.step(K, ordered=False)
+        for e, s_ in zip(ev1, streams):
+            e.record(s_)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         wall = time.perf_counter() - t0
-        dev_ms = ev0.elapsed_time(ev1)
+        dev_ms = max(a_.elapsed_time(b_) for a_ in ev0 for b_ in ev1)
         stop = eng.stop_iter.cpu().numpy()
         # executed iterations in the timed window [W+1, W+K] per replica
         last = np.where(stop == 0, W + K, stop - 1)
@@ -393,7 +400,7 @@ def main(argv=None):
                                "all_gather over every rank"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "time_base": "HIP events around the K timed iterations (device time per iteration)",
+                         "time_base": "HIP events on every replica group's stream around the K timed iterations, first start to last end (device time per iteration)",
                          "achieved_wall": achieved_wall, "frac_wall": achieved_wall / HBM_PEAK_GBS,
                          "traffic_unit": "bytes per iteration (all replicas), from "
                                          + (os.path.relpath(tfile, ROOT) if tfile else "no PMC traffic file"),

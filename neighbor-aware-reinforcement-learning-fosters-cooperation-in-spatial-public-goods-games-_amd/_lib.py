@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 GEN_ERR_SPIN = 1
 STATE_REPUTATION, STATE_ACTION = 0, 1
@@ -33,7 +33,7 @@ ST_SUMQ, ST_SUMQ_C, ST_SUMQ_D, ST_GMAX = 21, 25, 29, 33
 NSTAT = 34
 
 EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create", "spgg_set_params",
-            "spgg_bind", "spgg_step", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
+            "spgg_bind", "spgg_step", "spgg_step_groups", "spgg_flush", "spgg_draw", "spgg_payoff", "spgg_tile_shape",
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
             "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range",
             "spgg_mt_chains", "spgg_mt_jump_poly", "spgg_stream_create", "spgg_stream_destroy",
@@ -101,6 +101,8 @@ def load(path: str | None = None):
         lib.spgg_bind.argtypes = [vp, ctypes.POINTER(Buffers)]
         lib.spgg_step.restype = ctypes.c_int
         lib.spgg_step.argtypes = [vp, i32, i32, vp]
+        lib.spgg_step_groups.restype = ctypes.c_int
+        lib.spgg_step_groups.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i32, i32, i32]
         lib.spgg_flush.restype = ctypes.c_int
         lib.spgg_flush.argtypes = [vp, i32, vp]
         lib.spgg_history_finalize.restype = ctypes.c_int

@@ -49,11 +49,16 @@ using namespace spgg;
 //   8 = no history reductions (NCOOP kept constant), 64 = empty workgroups (launch floor),
 //   16 = no workgroup totals (final barrier + epilogue), 512 = no per-agent Q / md / atd loads
 //   (synthetic values), 2048 = no per-agent Q / md / atd stores, 8192 = no md loads / stores (the
-//   pending NI term reads +0), 4096 = Q plane 0 read only (plane 1's
+//   pending NI term reads +0), 16384 (with 8) = the lattice-wide max still recorded (the dynamics
+//   of the product), 32768 = no NI percent (its |alpha*td'| dead), 65536 = no phase-1b value
+//   reductions, 131072 = no counter reductions (NCOOP kept constant), 4096 = Q plane 0 read only (plane 1's
 //   entries copied from it), 128 = memory only (the owned loads,
 //   staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
+#endif
+#ifndef SPGG_QSTORE  // A/B probe: 0 changed rows, 1 both rows, 2 rows changed anywhere in the 8-agent line
+#define SPGG_QSTORE 0
 #endif
 // (Rejected A/B knobs -- reward-code pending records, partial Q stores, non-temporal
 // per-agent streams, wave priorities -- live in profiles/r02/rejected_knobs.patch with
@@ -1243,7 +1248,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
           // NI percent (spgg.py:512; x100 applied to the workgroup total), in f32:
           // a history mean (tolerance 1e-5), each term a ratio in [0, 1]
           const float anu = fabsf((float)nu);
-          pct = __builtin_fmaf(anu * __builtin_amdgcn_rcpf((atdv + anu) + 1e-8f), (float)vmu, pct);
+          pct = (SPGG_ABLATE & 32768) ? 0.f : __builtin_fmaf(anu * __builtin_amdgcn_rcpf((atdv + anu) + 1e-8f), (float)vmu, pct);
         }
         const double cm = ((b >> 3) & 1) ? 0.0 : vmu;                  // prev_S of t-1 == C
 #pragma unroll
@@ -1349,7 +1354,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     va[0] = (double)rsum;
     va[3] = (double)pct_t1;
     // red[wave*64 + 16..19]: va[0..3] (reduced here: frees their registers for phases 1c / 2)
-    if (!(SPGG_ABLATE & 8)) wave_partials<4>(va, red, 16);
+    if (!(SPGG_ABLATE & (8 | 65536))) wave_partials<4>(va, red, 16);
   }
   STAMP(3);
 
@@ -1431,8 +1436,17 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                                             act, sn, q[u], qb[u], &rn0, &rn1);
       if (diag_on && !(SPGG_ABLATE & (256 | 2048))) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
       // the rows this launch changed: the TD row (so) and the NI row of t-1 (phase 1a)
-      if (!(SPGG_ABLATE & 2048))
-        store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u], ((ni_rows >> (2 * u)) & 3u) | (1u << so));
+      if (!(SPGG_ABLATE & 2048)) {
+        uint32_t rows = ((ni_rows >> (2 * u)) & 3u) | (1u << so);
+#if SPGG_QSTORE == 1
+        rows = 3u;
+#elif SPGG_QSTORE == 2
+        rows |= (uint32_t)__shfl_xor((int)rows, 1);
+        rows |= (uint32_t)__shfl_xor((int)rows, 2);
+        rows |= (uint32_t)__shfl_xor((int)rows, 4);
+#endif
+        store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u], rows);
+      }
       // neighbour influence, spgg.py:477-494: first argmax wins ties
       const int w = ly.aw;
       constexpr int KN = M2 ? 12 : 4;
@@ -1488,7 +1502,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
   }
   STAMP(5);
-  if (!(SPGG_ABLATE & 8)) {  // red[wave*64 + 24..29]: counter words (fields of the layout above)
+  if (!(SPGG_ABLATE & (8 | 131072))) {  // red[wave*64 + 24..29]: counter words (fields of the layout above)
     uint32_t cw[8] = {cw0,
                       cw1,
                       nmd2 | ((gcn & 0xfu) << 16),
@@ -1511,7 +1525,15 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   STAMP(6);
 
   // ---- workgroup totals -> per-iteration history record ------------------
-  if ((SPGG_ABLATE & 8) && tid == 0 && tile == 0 && acting) srow[(size_t)(t + 1) * SPGG_NSTAT] = n / 2;
+  if ((SPGG_ABLATE & (8 | 131072)) && tid == 0 && tile == 0 && acting) srow[(size_t)(t + 1) * SPGG_NSTAT] = n / 2;
+  if ((SPGG_ABLATE & 16392) == 16392 && tid == 40 && acting) {  // 8 + 16384: the lattice max kept (dynamics unchanged)
+    double bm = 0.0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) bm = max_f64(bm, red[w * 64 + 12]);
+    if (bm > 0.0)
+      atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
+                (unsigned long long)__double_as_longlong(bm));
+  }
   if (tid < 64 && !(SPGG_ABLATE & 8)) {
     double tot[2] = {0.0, 0.0};  // this slot and (for derived values) its "C" partner
     int slot = -1, k = -1, src = -1, src_c = -1;
@@ -1547,6 +1569,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
                   (unsigned long long)__double_as_longlong(bm));
     }
+    if ((SPGG_ABLATE & 131072) && tid >= 19 && tid <= 29) slot = -1;  // (counter fields)
     if (slot >= 0) {
       const int j = tid - 16;
       const bool counter = j >= 3 && j <= 13;
@@ -2817,17 +2840,23 @@ int spgg_bind(spgg_ctx* c, const spgg_buffers* b) {
   return SPGG_OK;
 }
 
-int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
+// spgg_step's argument and state checks (no side effects: spgg_step_groups checks every
+// context before it enqueues anything).
+static int step_check(spgg_ctx* c, int32_t t0, int32_t n_steps) {
   if (!c) return SPGG_E_ARG;
   if (!c->bound || !c->params_set) return fail(c, SPGG_E_STATE, "spgg_step before bind/set_params");
   if (t0 < 1 || n_steps < 0 || (long long)t0 + n_steps - 1 > c->cfg.iterations)
     return fail(c, SPGG_E_ARG, "spgg_step: iteration range outside [1, iterations]");
   if (c->cfg.rng_mode == SPGG_RNG_INJECT && n_steps > 1)
     return fail(c, SPGG_E_ARG, "spgg_step: INJECT mode steps one iteration per call");
-  if (t0 == 1) c->kappa_woke = false;  // a new run
-  else if (c->kappa_woke)
+  if (t0 != 1 && c->kappa_woke)
     return fail(c, SPGG_E_STATE, "spgg_step: a replica's kappa changed from 0 to nonzero mid-run");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return SPGG_OK;
+}
+
+// Run setup of a checked spgg_step call: the iteration-1 prologue and the generator's start.
+static int step_begin(spgg_ctx* c, int32_t t0, int32_t n_steps, hipStream_t s) {
+  if (t0 == 1) c->kappa_woke = false;  // a new run
   const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
   if (mt) {
     int rc = mt_lazy_init(c);
@@ -2835,10 +2864,6 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
     if (t0 == 1) c->gen_upto = 0;  // a new run: generation restarts from mt_state
   }
   if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
-  const int K = c->gen_chunk, T = c->cfg.iterations;
-  // timing-only builds (-DSPGG_TIMING=1: the step launches skipped, the generator alone; =2: the
-  // generator launches skipped, steps on stale draws; results are WRONG); 0 in the product
-  constexpr int timing = SPGG_TIMING;
   if (mt && n_steps > 0 && c->gen_upto == 0) {
     // a run's first generator chunks read mt_state, eps and stop_iter and write the draw and
     // snapshot rings, which the caller may have just written on its own stream (e.g. torch's
@@ -2846,17 +2871,54 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
     (void)hipEventRecord(c->caller_ready, s);
     (void)hipStreamWaitEvent(c->gen_stream, c->caller_ready, 0);
   }
-  for (int t = t0; t < t0 + n_steps; ++t) {
-    if (mt) {
-      const int q = (t - 1) / K;
-      // this chunk and the next one enqueued (the next overlaps this chunk's steps)
-      while (timing != 2 && c->gen_upto < std::min(T, (q + 2) * K)) enqueue_gen_chunk(c, c->gen_upto / K);
-      if (timing != 2 && (t == q * K + 1 || t == t0)) (void)hipStreamWaitEvent(s, c->gen_done[q & 1], 0);
-    }
-    if (timing != 1) launch_step(c, t, 0, s);
-    if (mt && (t % K == 0 || t == T)) (void)hipEventRecord(c->step_done[((t - 1) / K) & 1], s);
+  return SPGG_OK;
+}
+
+// Iteration t of a spgg_step call that began at t0: its generator chunks (MT19937) and the
+// step launch.
+static void step_iter(spgg_ctx* c, int t, int32_t t0, hipStream_t s) {
+  const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
+  const int K = c->gen_chunk, T = c->cfg.iterations;
+  // timing-only builds (-DSPGG_TIMING=1: the step launches skipped, the generator alone; =2: the
+  // generator launches skipped, steps on stale draws; results are WRONG); 0 in the product
+  constexpr int timing = SPGG_TIMING;
+  if (mt) {
+    const int q = (t - 1) / K;
+    // this chunk and the next one enqueued (the next overlaps this chunk's steps)
+    while (timing != 2 && c->gen_upto < std::min(T, (q + 2) * K)) enqueue_gen_chunk(c, c->gen_upto / K);
+    if (timing != 2 && (t == q * K + 1 || t == t0)) (void)hipStreamWaitEvent(s, c->gen_done[q & 1], 0);
   }
+  if (timing != 1) launch_step(c, t, 0, s);
+  if (mt && (t % K == 0 || t == T)) (void)hipEventRecord(c->step_done[((t - 1) / K) & 1], s);
+}
+
+int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
+  int rc = step_check(c, t0, n_steps);
+  if (rc) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if ((rc = step_begin(c, t0, n_steps, s))) return rc;
+  for (int t = t0; t < t0 + n_steps; ++t) step_iter(c, t, t0, s);
   return hip_check(c, hipGetLastError(), "spgg_step launch");
+}
+
+int spgg_step_groups(spgg_ctx* const* ctxs, void* const* streams, int32_t n_ctx, int32_t t0, int32_t n_steps) {
+  if (!ctxs || !streams || n_ctx < 1) return SPGG_E_ARG;
+  for (int i = 0; i < n_ctx; ++i) {
+    if (!ctxs[i]) return SPGG_E_ARG;
+    for (int j = 0; j < i; ++j)
+      if (ctxs[j] == ctxs[i]) return fail(ctxs[i], SPGG_E_ARG, "spgg_step_groups: a context listed twice");
+    if (ctxs[i]->cfg.rng_mode == SPGG_RNG_INJECT)
+      return fail(ctxs[i], SPGG_E_ARG, "spgg_step_groups: INJECT mode steps through spgg_step");
+    int rc = step_check(ctxs[i], t0, n_steps);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < n_ctx; ++i) {
+    int rc = step_begin(ctxs[i], t0, n_steps, reinterpret_cast<hipStream_t>(streams[i]));
+    if (rc) return rc;
+  }
+  for (int t = t0; t < t0 + n_steps; ++t)
+    for (int i = 0; i < n_ctx; ++i) step_iter(ctxs[i], t, t0, reinterpret_cast<hipStream_t>(streams[i]));
+  return hip_check(ctxs[0], hipGetLastError(), "spgg_step_groups launch");
 }
 
 int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {

@@ -300,6 +300,9 @@ class BatchEngine:
         self.cache_bytes = int(float(os.environ.get("SPGG_CACHE_MB", "240")) * 2**20)
         self.chunk = max(1, int(os.environ.get("SPGG_CHUNK", "64")))
         self.enqueue_chunk = int(os.environ.get("SPGG_ENQ_CHUNK", "8"))
+        # resident replica groups enqueued iteration by iteration in one call (spgg_step_groups);
+        # SPGG_INTERLEAVE=0: one spgg_step call per group and enqueue_chunk iterations
+        self.interleave = os.environ.get("SPGG_INTERLEAVE", "1") != "0"
         self.skip_dead = os.environ.get("SPGG_SKIP_DEAD", "1") != "0"
         if streams is None and os.environ.get("SPGG_STREAMS"):
             streams = int(os.environ["SPGG_STREAMS"]) or None
@@ -553,8 +556,21 @@ class BatchEngine:
         rec = np.ascontiguousarray(words.transpose(1, 2, 0)).reshape(self.R, -1)
         self.draws[(t - 1) % self.draw_slots].copy_(torch.from_numpy(rec.view(np.int32)))
 
-    def step(self, n_steps: int):
-        """Enqueue the next n_steps iterations (no host sync except in inject mode)."""
+    def launch_streams(self):
+        """The torch streams this engine's step launches run on: the replica groups' streams, or
+        the current stream for a single group (for events recorded beside the launches)."""
+        if self.G == 1:
+            return [torch.cuda.current_stream(self.dev)]
+        return list(self.streams)
+
+    def step(self, n_steps: int, ordered: bool = True):
+        """Enqueue the next n_steps iterations (no host sync except in inject mode).
+
+        ordered=False (every group resident): the groups' streams are NOT ordered after the
+        current stream's earlier work nor it after theirs -- for a caller that has synchronised
+        the device before and synchronises it after (bench.py's timed window).  Each of those two
+        cross-stream waits costs a window ~60 us of latency on MI355X / ROCm 7 (cfg3, 20
+        iterations: 63.4 -> 57.1 us/step without both; tools/window_timeline.py)."""
         n_steps = min(n_steps, self.T - self.t + 1)
         if n_steps <= 0:
             return 0
@@ -565,6 +581,25 @@ class BatchEngine:
                 self.t += 1
         else:
             t0, end = self.t, self.t + n_steps
+            live = [g for g in self.groups if g["live"]]
+            if self.G > 1 and self.resident == self.G and self.interleave and live:
+                # every group resident: one call enqueues all of them iteration by iteration
+                # (spgg_step_groups), so every group's stream starts within one launch of the
+                # first instead of one host call of k launches per group later (cfg3, 20
+                # iterations after 400: 60.0 -> 57.8 us/step for k = 8 -> 1)
+                ctxs = (ctypes.c_void_p * len(live))(*[g["ctx"] for g in live])
+                strs = (ctypes.c_void_p * len(live))(*[g["stream"].cuda_stream for g in live])
+                cur = torch.cuda.current_stream(self.dev)  # ordered as _enqueue orders its rounds
+                if ordered:
+                    for st in self.streams:
+                        st.wait_stream(cur)
+                C.check(self.lib.spgg_step_groups(ctxs, strs, len(live), t0, n_steps), live[0]["ctx"],
+                        "spgg_step_groups")
+                if ordered:
+                    for st in self.streams:
+                        cur.wait_stream(st)
+                self.t += n_steps
+                return n_steps
             # groups are enqueued round-robin, k iterations at a time: with every group
             # resident this only interleaves the host's launches across the streams (all
             # of them start within k launches, instead of the last group waiting for the

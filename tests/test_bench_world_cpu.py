@@ -52,7 +52,10 @@ def _worker(rank, world, port, q):
             self.t = 1
             FakeEngine.made.append(dict(offset=replica_offset, R=self.R, T=iterations))
 
-        def step(self, n):
+        def launch_streams(self):
+            return [None]
+
+        def step(self, n, ordered=True):
             time.sleep(0.02 * n * (1 + rank))
             for t in range(self.t, self.t + n):      # a cooperation count per iteration: 100*rank + t
                 self.st[:, t + 1, C.ST_NCOOP] = 100 * rank + t

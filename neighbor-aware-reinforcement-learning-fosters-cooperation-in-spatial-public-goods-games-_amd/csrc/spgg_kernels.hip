@@ -2769,7 +2769,9 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   c->tiles_per_rep = c->tiles_x * ((cfg->L + c->TH - 1) / c->TH);
   // history-record stripes: <= kTilesPerStripe workgroups add to one record address per
   // iteration (a single record of an L=1000 replica took 1000 atomics per address: ~12 us)
-  while (c->stripes < 32 && (c->tiles_per_rep + c->stripes - 1) / c->stripes > kTilesPerStripe) c->stripes *= 2;
+  int tiles_per_stripe = kTilesPerStripe;
+  if (const char* e = getenv("SPGG_TILES_PER_STRIPE")) tiles_per_stripe = std::max(1, atoi(e));
+  while (c->stripes < 32 && (c->tiles_per_rep + c->stripes - 1) / c->stripes > tiles_per_stripe) c->stripes *= 2;
   const int HA = cfg->second_order ? 2 : 1;
   const bool twc = twc_of(*cfg, c->TW, c->TH) > 0;
   const LdsLayout ly = lds_layout(c->TW, c->TH, HA + 2, HA, cfg->rep_int8 ? 1 : 8, twc,

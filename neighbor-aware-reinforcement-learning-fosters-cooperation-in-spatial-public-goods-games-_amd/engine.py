@@ -587,8 +587,11 @@ class BatchEngine:
                 # (spgg_step_groups), so every group's stream starts within one launch of the
                 # first instead of one host call of k launches per group later (cfg3, 20
                 # iterations after 400: 60.0 -> 57.8 us/step for k = 8 -> 1)
-                ctxs = (ctypes.c_void_p * len(live))(*[g["ctx"] for g in live])
-                strs = (ctypes.c_void_p * len(live))(*[g["stream"].cuda_stream for g in live])
+                key = tuple(id(g) for g in live)   # the call's arrays, made once per live set
+                if getattr(self, "_groups_args", (None,))[0] != key:
+                    self._groups_args = (key, (ctypes.c_void_p * len(live))(*[g["ctx"] for g in live]),
+                                         (ctypes.c_void_p * len(live))(*[g["stream"].cuda_stream for g in live]))
+                _, ctxs, strs = self._groups_args
                 cur = torch.cuda.current_stream(self.dev)  # ordered as _enqueue orders its rounds
                 if ordered:
                     for st in self.streams:

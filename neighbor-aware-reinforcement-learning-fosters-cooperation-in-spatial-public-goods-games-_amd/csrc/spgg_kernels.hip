@@ -841,8 +841,8 @@ constexpr int kStampWG = 8192;
 __device__ unsigned long long spgg_stamps[kStampWG * 10];
 #define STAMP(k)                                                                            \
   do {                                                                                      \
-    if (t == SPGG_STAMP_T && tid == 0 && logical < kStampWG)                                \
-      spgg_stamps[logical * 10 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
+    if (t == SPGG_STAMP_T && tid == 0 && stamp_id < kStampWG)                               \
+      spgg_stamps[stamp_id * 10 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
   } while (0)
 #else
 #define STAMP(k) \
@@ -887,6 +887,11 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (SPGG_ABLATE & 64) return;
   const int rep = logical / a.tiles_per_rep;
   const int tile = logical - rep * a.tiles_per_rep;
+#if SPGG_STAMPS
+  // the workgroup's stamp slot: the batch-wide replica id (stream_id) and tile, so the launches of
+  // every replica group (stream) of a batch stamp disjoint slots
+  const int stamp_id = (int)a.params[rep].stream_id * a.tiles_per_rep + tile;
+#endif
 
   const int L = a.L, n = a.n;
   const bool tiny = TWC ? false : L < 8;  // TWC => L % TWC == 0
@@ -930,12 +935,12 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
   STAMP(0);
 #if SPGG_STAMPS
-  if (t == SPGG_STAMP_T && tid == 0 && logical < kStampWG) {
+  if (t == SPGG_STAMP_T && tid == 0 && stamp_id < kStampWG) {
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    spgg_stamps[logical * 10 + 8] = hw;
-    spgg_stamps[logical * 10 + 9] = xcc;
+    spgg_stamps[stamp_id * 10 + 8] = hw;
+    spgg_stamps[stamp_id * 10 + 9] = xcc;
   }
 #endif
 

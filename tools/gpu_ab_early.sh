@@ -9,7 +9,7 @@ R=$1; read W K <<< "$2"; shift 2
 for r in $(seq $R); do
   for L in "$@"; do
     tag=$(basename "$L" .so)
-    timeout -k 10 120 python tools/ab.py --libs "$L" --warmup $W --steps $K --rounds 2 --clock $((K * 50)) > "$O/tmp.txt" 2>&1 || { tail -3 "$O/tmp.txt"; exit 1; }
+    timeout -k 10 120 python tools/ab.py --config ${CONFIG:-cfg3} --libs "$L" --warmup $W --steps $K --rounds 2 --clock $((K * 50)) > "$O/tmp.txt" 2>&1 || { tail -3 "$O/tmp.txt"; exit 1; }
     grep median "$O/tmp.txt" | sed "s/^/$r /" >> "$O/ab_w${W}_k${K}.txt"
   done
 done

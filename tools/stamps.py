@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--t", type=int, default=30)
     ap.add_argument("--rng", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--streams", type=int, default=1, help="replica groups (the bench's: 0 = the planner's)")
     args = ap.parse_args()
     import torch
     import bench
@@ -29,7 +30,7 @@ def main():
     desc, L, M2, state, reps = bench.workload(args.config, 0)
     lib = os.path.abspath(args.lib)
     eng = BatchEngine(L, args.t + 5, reps, use_second_order=M2, state_representation=state, rng=args.rng,
-                      lib_path=lib, streams=1)
+                      lib_path=lib, streams=args.streams or None)
     eng.step(args.t + 2)
     torch.cuda.synchronize()
     h = ctypes.CDLL(lib)
@@ -43,7 +44,7 @@ def main():
     s = s[s[:, 0] > 0]
     t0 = s[:, 0].min()
     st = (s[:, :8] - t0) * 10 / 1000.0  # us
-    print(f"workgroups stamped {len(s)}; launch span {st[:, 7].max():.1f} us")
+    print(f"workgroups stamped {len(s)} (iteration {args.t}, {eng.resident} stream(s)); span {st[:, 7].max():.1f} us")
     names = ["loads+staging", "PC+1a", "barrier+1b", "1c+barrier", "phase2", "red barrier", "totals+atomics"]
     d = np.diff(st, axis=1)
     print("phase            mean   p10   p50   p90  (us per workgroup)")

@@ -403,36 +403,43 @@ def test_replica_groups_on_streams_match_single_stream(rng, alg):
 @pytest.mark.parametrize("rng", ["philox", "mt19937"])
 def test_interleaved_group_enqueue_matches_per_group_calls(rng):
     """spgg_step_groups (every group enqueued iteration by iteration in one call, the engine's
-    default with every group resident) gives bit-identical lattices, records and MT keys to one
-    spgg_step call per group; it refuses a context listed twice."""
+    default with every group resident), also unordered against the caller's stream between
+    device synchronisations (bench.py's window), gives bit-identical lattices, records and MT keys
+    to one spgg_step call per group; it refuses a context listed twice."""
     import ctypes
     from spgg_amd import _lib as C
     L, T = 30, 70
     reps = [_runner_params(r=2.0 + 0.25 * s, seed=s) for s in range(6)]
     res = {}
-    for inter in (False, True):
+    for inter in (False, True, "unordered"):
         eng = BatchEngine(L, T, reps, use_second_order=False, rng=rng, streams=3)
-        eng.interleave = inter
+        eng.interleave = bool(inter)
         eng.enqueue_chunk = 8
         done = 0
         for k in (1, 5, 64):  # ragged calls, across an MT19937 generator chunk
-            done += eng.step(min(k, T - done))
+            if inter == "unordered":  # bench.py's window: the device synchronised around each call
+                torch.cuda.synchronize()
+                done += eng.step(min(k, T - done), ordered=False)
+                torch.cuda.synchronize()
+            else:
+                done += eng.step(min(k, T - done))
         eng.flush()
         torch.cuda.synchronize()
         res[inter] = ([eng.final_state(k) for k in range(len(reps))], eng.stats_folded().cpu().numpy(),
                       eng.mt_state.cpu().numpy().copy() if rng == "mt19937" else None)
-        if inter:
+        if inter is True:
             g = eng.groups[0]
             ctxs = (ctypes.c_void_p * 2)(g["ctx"], g["ctx"])
             strs = (ctypes.c_void_p * 2)(g["stream"].cuda_stream, g["stream"].cuda_stream)
             assert eng.lib.spgg_step_groups(ctxs, strs, 2, 1, 1) == C.E_ARG
         eng.close()
-    for a, b in zip(res[False][0], res[True][0]):
-        for x, y in zip(a, b):
-            assert np.array_equal(x, y)
-    np.testing.assert_allclose(res[False][1], res[True][1], rtol=1e-12, atol=1e-12)
-    if rng == "mt19937":
-        assert np.array_equal(res[False][2], res[True][2])
+    for other in (True, "unordered"):
+        for a, b in zip(res[False][0], res[other][0]):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y)
+        np.testing.assert_allclose(res[False][1], res[other][1], rtol=1e-12, atol=1e-12)
+        if rng == "mt19937":
+            assert np.array_equal(res[False][2], res[other][2])
 
 
 @pytest.mark.parametrize("rng", ["philox", "mt19937"])

@@ -7,7 +7,7 @@ R=$1; shift
 for r in $(seq $R); do
   for E in "$@"; do
     if [ "$E" = "-" ]; then A=(); else A=($E); fi
-    timeout -k 10 200 env "${A[@]}" python bench.py --no-cpu-baseline --no-mt --full-run 0 > "$O/tmp.json" 2> "$O/tmp.err" || { tail -3 "$O/tmp.err"; exit 1; }
+    timeout -k 10 200 env "${A[@]}" python bench.py --config ${CONFIG:-cfg3} --no-cpu-baseline --no-mt --full-run 0 > "$O/tmp.json" 2> "$O/tmp.err" || { tail -3 "$O/tmp.err"; exit 1; }
     python -c "
 import json; d=json.loads(open('$O/tmp.json').read().strip().splitlines()[-1])
 print('$r', '$E'.replace(' ', ','), '%.2f %.2f %.2f' % (d['ms_per_step']*1e3, d['roofline']['device_ms_per_step']*1e3, d['steady_window']['ms_per_step']*1e3))" >> "$O/ab.txt"

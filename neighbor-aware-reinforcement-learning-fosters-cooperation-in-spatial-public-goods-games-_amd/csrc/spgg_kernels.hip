@@ -790,10 +790,13 @@ __device__ __forceinline__ double prev_max_diff(const double* rew, int ca, int w
   double rw[KN];
 #pragma unroll
   for (int k = 0; k < KN; ++k) rw[k] = rew[nb[k]];
-  double md = rw[0] - r0;
+  // max_k RN(rw_k - r0) = RN(max_k rw_k - r0): x -> RN(x - r0) is non-decreasing and the maximum
+  // attains it, so one subtraction gives phase 2's value bit for bit (phase 2 needs every
+  // difference: its argmax keeps the first of equal rounded differences)
+  double m = rw[0];
 #pragma unroll
-  for (int k = 1; k < KN; ++k) md = max_f64(md, rw[k] - r0);
-  return max_f64(md, 0.0);  // max(0, md): one v_max_f64 (md is never -0)
+  for (int k = 1; k < KN; ++k) m = max_f64(m, rw[k]);
+  return max_f64(m - r0, 0.0);  // max(0, md): one v_max_f64 (md is never -0)
 }
 
 // |diag_alpha * td'| of iteration t-1 (spgg.py:446-475) from the table after its TD update
@@ -1401,10 +1404,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int act = ex ? rbt : (QB ? greedy2(mean2(v0, w0), mean2(v1, w1)) : greedy2(v0, v1));
       const RVal<RQ> rn = rep_next<RQ>(r_t, act, hp);
       const double rr = act == 0 ? 0.5 : 0.0;
-      const double wpp = w_p * P, wrr = w_rep * rr;
       const int ca = ay * ly.aw + ax;
       sA[ca] = (uint8_t)act;
       sRn[ca] = (RT)rn;
+      const double wpp = w_p * P, wrr = w_rep * rr;
       sRew[ca] = wpp + wrr;
     }
   }
@@ -1540,8 +1543,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                 (unsigned long long)__double_as_longlong(bm));
   }
   if (tid < 64 && !(SPGG_ABLATE & 8)) {
-    double tot[2] = {0.0, 0.0};  // this slot and (for derived values) its "C" partner
-    int slot = -1, k = -1, src = -1, src_c = -1;
+    // lane -> record value: source word src of every wave's red[] (and, for derived values, its
+    // "C" partner src_c); lane 40 reads the wave maxima (word 12) for the lattice-wide max
+    int slot = -1, k = -1, src = 12, src_c = -1;
+    bool counter = false;
     // Finalize group (slot t-1): sums over prev-D are total - prev-C.
     if (tid < 13) {
       if (pending) {
@@ -1561,33 +1566,43 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       constexpr uint64_t km1 = stat_bytes(SPGG_ST_GC0, SPGG_ST_GC0 + 1, SPGG_ST_GC0 + 2, SPGG_ST_GC0 + 3,
                                           SPGG_ST_GC0 + 4, SPGG_ST_GC0 + 5, -1, -1);
       k = (int)(int8_t)(uint8_t)((j < 8 ? km0 : km1) >> (8 * (j & 7)));
-      src = 16 + j;
+      counter = j >= 3;
+      src = counter ? 24 + ((j - 3) >> 1) : 16 + j;
       const bool start_val = j == 0;                   // recorded on the absorbing iteration too
       if ((acting || start_val) && k >= 0) slot = (j == 5) ? t + 1 : t;
     }
+    if ((SPGG_ABLATE & 131072) && tid >= 19 && tid <= 29) slot = -1;  // (counter fields)
+    // every word of the four waves read at once, unconditionally: one LDS round trip (the reads
+    // chained under the derived values' branches held the workgroup's last wave, and with it the
+    // CU's slot for the next workgroup, ~0.9 us)
+    const int sc = src_c >= 0 ? src_c : src;
+    double x[kWaves], y[kWaves];
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      x[w] = red[w * 64 + src];
+      y[w] = red[w * 64 + sc];
+    }
+    const double rep_unit = hp.rep_unit;  // (from LDS: a global read here would wait for every store of the tile)
     if (tid == 40 && acting) {  // lattice-wide max |diff| (spgg.py:488)
       double bm = 0.0;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) bm = max_f64(bm, red[w * 64 + 12]);
+      for (int w = 0; w < kWaves; ++w) bm = max_f64(bm, x[w]);
       // non-negative doubles order like their bit patterns
       if (bm > 0.0)
         atomicMax(reinterpret_cast<unsigned long long*>(&srow[(size_t)t * SPGG_NSTAT + SPGG_ST_GMAX]),
                   (unsigned long long)__double_as_longlong(bm));
     }
-    if ((SPGG_ABLATE & 131072) && tid >= 19 && tid <= 29) slot = -1;  // (counter fields)
     if (slot >= 0) {
       const int j = tid - 16;
-      const bool counter = j >= 3 && j <= 13;
-      const int word = 24 + ((j - 3) >> 1);
+      double tot0 = 0.0, tot1 = 0.0;  // this slot and (for derived values) its "C" partner
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) {
-        tot[0] += red[w * 64 + (counter ? word : src)];
-        if (src_c >= 0) tot[1] += red[w * 64 + src_c];
+        tot0 += x[w];
+        tot1 += y[w];
       }
-      double val = src_c >= 0 ? tot[0] - tot[1] : tot[0];
-      if (counter) val = (double)(((unsigned long long)tot[0] >> (16 * ((j - 3) & 1))) & 0xffffu);
-      // (from LDS: a global read here would wait for every store of the tile)
-      if (RQ && k == SPGG_ST_SUMR) val *= hp.rep_unit;
+      double val = src_c >= 0 ? tot0 - tot1 : tot0;
+      if (counter) val = (double)(((unsigned long long)tot0 >> (16 * ((j - 3) & 1))) & 0xffffu);
+      if (RQ && k == SPGG_ST_SUMR) val *= rep_unit;
       if (k == SPGG_ST_SUM_PCT || k == SPGG_ST_SUM_RATIO_C) val *= 100.0;  // percent sums
       if (val != 0.0 && (!(SPGG_ABLATE & 2) || k == SPGG_ST_NCOOP))
         atomicAdd(&srow[(size_t)slot * SPGG_NSTAT + k], val);

@@ -6,7 +6,7 @@ R=$1; C=$2; N=$3; shift 3
 for r in $(seq $R); do
   for E in "$@"; do
     if [ "$E" = "-" ]; then A=(); else A=($E); fi
-    timeout -k 10 200 env "${A[@]}" python tools/fullrun_probe.py --config $C --rng philox --iters $N > "$O/tmp.txt" 2>&1 || { tail -3 "$O/tmp.txt"; exit 1; }
+    timeout -k 10 200 env "${A[@]}" python tools/fullrun_probe.py --config $C --rng ${RNG:-philox} --iters $N > "$O/tmp.txt" 2>&1 || { tail -3 "$O/tmp.txt"; exit 1; }
     echo "$r $C $E $(tail -1 $O/tmp.txt)" >> "$O/fr.txt"
   done
 done

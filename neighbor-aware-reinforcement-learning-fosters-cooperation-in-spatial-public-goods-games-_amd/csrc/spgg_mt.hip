@@ -147,7 +147,17 @@ void jump_poly(uint64_t e, uint32_t* out) {
       std::memset(out, 0, kKey * sizeof(uint32_t));
       return;
     }
-    it = cache.emplace(e, pow_x(e)).first;
+    // the generator's jump levels are e_{j+1} = 2 e_j + 1 (jumps of D << j words, minus one):
+    // x^(2e+1) = (x^e)^2 x mod phi, one squaring instead of a whole exponentiation (~35 ms each)
+    auto half = (e & 1u) ? cache.find(e >> 1) : cache.end();
+    if (half != cache.end()) {
+      Poly p = half->second;
+      sqr_mod(p);
+      mulx_mod(p);
+      it = cache.emplace(e, std::move(p)).first;
+    } else {
+      it = cache.emplace(e, pow_x(e)).first;
+    }
   }
   std::memcpy(out, it->second.data(), kKey * sizeof(uint32_t));  // 312 u64 = 624 u32 (little endian)
 }

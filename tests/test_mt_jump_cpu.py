@@ -110,3 +110,18 @@ def test_tempered_low_bit_is_a_parity_of_raw_bits():
     for b in range(32):
         par ^= (z >> np.uint32(b)) & np.uint32(1)
     assert np.array_equal(_temper(y) & np.uint32(1), par)
+
+
+def test_doubled_jumps_derived_by_squaring():
+    """The generator's jump levels D << j (polynomial exponents 2e + 1 of the level below) are
+    derived from the cached level by one squaring and one multiplication by x
+    (spgg_mt.hip jump_poly); each still moves a window by exactly its distance."""
+    rs = np.random.RandomState(2024)
+    key = np.asarray(rs.get_state()[1], dtype=np.uint32)
+    D = 12_347
+    x = _stream(key, (D << 2) + 624 + 1)
+    j = np.arange(624)
+    for lvl in range(3):          # level 0 exponentiated, levels 1 and 2 derived from it
+        Dl = D << lvl
+        got = np.bitwise_xor.reduce(x[1 + _poly(Dl - 1)[:, None] + j[None, :]], axis=0)
+        assert np.array_equal(got, x[Dl: Dl + 624]), lvl

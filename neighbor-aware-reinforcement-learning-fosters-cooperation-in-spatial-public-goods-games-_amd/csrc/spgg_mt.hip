@@ -93,9 +93,47 @@ const Poly& phi() {
   return p;
 }
 
+// Reduction table: T[v] (v < 256) = the multiple m * phi (deg m < 8) whose coefficients at
+// degrees kDeg .. kDeg+7 are the bits of v and whose other coefficients lie below kDeg:
+// XOR-ing T[v] << s clears the eight coefficients kDeg+s .. kDeg+s+7 of a product at once
+// (a bit at a time took ~35 ms per exponentiation)
+constexpr int kTW = kPW + 1;  // words of a table entry (degree <= kDeg + 7)
+const std::vector<uint64_t>& red_table() {
+  static const std::vector<uint64_t> T = [] {
+    const Poly& f = phi();
+    std::vector<uint64_t> t(256 * kTW, 0);
+    // single bits first: phi << i, its coefficients kDeg .. kDeg+i-1 cleared with lower bits
+    for (int i = 0; i < 8; ++i) {
+      uint64_t* e = t.data() + (size_t)(1 << i) * kTW;
+      xor_shifted(e, f.data(), kPW, i);
+      for (int j = i - 1; j >= 0; --j)
+        if (bit_of(e, kDeg + j))
+          for (int w = 0; w < kTW; ++w) e[w] ^= t[(size_t)(1 << j) * kTW + w];
+    }
+    for (int v = 1; v < 256; ++v) {  // linear: T[v] = XOR of its single-bit entries
+      if ((v & (v - 1)) == 0) continue;
+      const int lo = v & -v;
+      for (int w = 0; w < kTW; ++w) t[(size_t)v * kTW + w] = t[(size_t)lo * kTW + w] ^ t[(size_t)(v ^ lo) * kTW + w];
+    }
+    return t;
+  }();
+  return T;
+}
+
+// q (degree <= 2 (kDeg - 1), 2 kPW + 2 words) mod phi, eight coefficients at a time from the top
+void reduce_mod(std::vector<uint64_t>& q) {
+  const std::vector<uint64_t>& T = red_table();
+  for (int s = 2 * (kDeg - 1) - kDeg - 7; s > -8; s -= 8) {
+    const int lo = s < 0 ? 0 : s;               // (the last chunk is narrower)
+    const int d = kDeg + lo, nb = s < 0 ? 8 + s : 8;
+    uint32_t v = 0;
+    for (int b = 0; b < nb; ++b) v |= (uint32_t)bit_of(q.data(), d + b) << b;
+    if (v) xor_shifted(q.data(), T.data() + (size_t)v * kTW, kTW, lo);
+  }
+}
+
 // p (degree < 19937) squared mod phi
 void sqr_mod(Poly& p) {
-  const Poly& f = phi();
   std::vector<uint64_t> q(2 * kPW + 2, 0);
   for (int w = 0; w < kPW; ++w) {
     uint64_t lo = 0, hi = 0;
@@ -107,8 +145,7 @@ void sqr_mod(Poly& p) {
     q[2 * w] = lo;
     q[2 * w + 1] = hi;
   }
-  for (int k = 2 * (kDeg - 1); k >= kDeg; --k)
-    if (bit_of(q.data(), k)) xor_shifted(q.data(), f.data(), kPW, k - kDeg);
+  reduce_mod(q);
   for (int w = 0; w < kPW; ++w) p[w] = q[w];
 }
 

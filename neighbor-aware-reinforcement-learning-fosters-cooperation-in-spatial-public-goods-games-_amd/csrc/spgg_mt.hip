@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace spgg_mt {
@@ -88,9 +89,10 @@ Poly derive_phi() {
   return phi;
 }
 
+// (heap objects never freed: the warm-up thread below may still run at process exit)
 const Poly& phi() {
-  static const Poly p = derive_phi();
-  return p;
+  static const Poly* p = new Poly(derive_phi());
+  return *p;
 }
 
 // Reduction table: T[v] (v < 256) = the multiple m * phi (deg m < 8) whose coefficients at
@@ -99,7 +101,7 @@ const Poly& phi() {
 // (a bit at a time took ~35 ms per exponentiation)
 constexpr int kTW = kPW + 1;  // words of a table entry (degree <= kDeg + 7)
 const std::vector<uint64_t>& red_table() {
-  static const std::vector<uint64_t> T = [] {
+  static const std::vector<uint64_t>* T = new std::vector<uint64_t>([] {
     const Poly& f = phi();
     std::vector<uint64_t> t(256 * kTW, 0);
     // single bits first: phi << i, its coefficients kDeg .. kDeg+i-1 cleared with lower bits
@@ -116,9 +118,22 @@ const std::vector<uint64_t>& red_table() {
       for (int w = 0; w < kTW; ++w) t[(size_t)v * kTW + w] = t[(size_t)lo * kTW + w] ^ t[(size_t)(v ^ lo) * kTW + w];
     }
     return t;
-  }();
-  return T;
+  }());
+  return *T;
 }
+
+// phi (Berlekamp-Massey, ~30 ms) and the reduction table built on a thread of their own when the
+// library loads: a run's first MT19937 launch (spgg_step's jump polynomials) finds them ready
+// instead of paying for them on the host before its first step (the function-local statics make
+// a caller that comes first wait for the same initialisation)
+struct MtHostWarmup {
+  MtHostWarmup() {
+    try {
+      std::thread([] { (void)red_table(); }).detach();
+    } catch (...) {  // no thread: built on first use
+    }
+  }
+} mt_host_warmup;
 
 // q (degree <= 2 (kDeg - 1), 2 kPW + 2 words) mod phi, eight coefficients at a time from the top
 void reduce_mod(std::vector<uint64_t>& q) {

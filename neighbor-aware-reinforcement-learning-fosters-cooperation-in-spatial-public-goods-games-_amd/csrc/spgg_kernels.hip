@@ -36,6 +36,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "spgg_abi.h"
@@ -2403,6 +2404,20 @@ void choose_mt_chains(spgg_ctx* c) {
   c->gen_chunk = chains * per;
   c->jump_levels = 0;
   while ((1 << c->jump_levels) < chains) ++c->jump_levels;
+  if (chains > 1) {
+    // the jump polynomials the first spgg_step needs (mt_lazy_init), computed now on a thread of
+    // their own: jump_poly caches them per exponent under its lock, so the step's calls find them
+    // ready, or wait for this computation instead of repeating it
+    const uint64_t D = (uint64_t)per * (uint64_t)W;
+    const int J = c->jump_levels;
+    try {
+      std::thread([D, J] {
+        uint32_t tmp[624];
+        for (int j = 0; j <= J; ++j) spgg_mt::jump_poly((D << j) - 1, tmp);
+      }).detach();
+    } catch (...) {  // no thread: computed by the first step
+    }
+  }
 }
 
 // Workgroups per history-record stripe (spgg_stat_stripes).

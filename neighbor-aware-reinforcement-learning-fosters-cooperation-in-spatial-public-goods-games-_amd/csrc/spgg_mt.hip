@@ -190,8 +190,11 @@ Poly pow_x(uint64_t e) {
 }  // namespace
 
 void jump_poly(uint64_t e, uint32_t* out) {
-  static std::mutex mu;
-  static std::map<uint64_t, Poly> cache;
+  // (never destroyed: a prefetching thread, spgg_create's, may still hold them at process exit)
+  static std::mutex* mu_p = new std::mutex;
+  static std::map<uint64_t, Poly>* cache_p = new std::map<uint64_t, Poly>;
+  std::mutex& mu = *mu_p;
+  std::map<uint64_t, Poly>& cache = *cache_p;
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache.find(e);
   if (it == cache.end()) {

@@ -37,7 +37,9 @@ EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
             "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range",
             "spgg_mt_chains", "spgg_mt_jump_poly", "spgg_stream_create", "spgg_stream_destroy",
-            "spgg_status", "spgg_test_set_error")
+            "spgg_status")
+# test-only entry points (include/spgg_test.h): exported by the library, not part of the product ABI
+TEST_EXPORTED = ("spgg_test_set_error",)
 
 
 class Config(ctypes.Structure):

@@ -29,7 +29,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-munsafe-fp-atomics"]
 
 
-DEPS = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h"),
+DEPS = SRC + [os.path.join(INC, "spgg_abi.h"), os.path.join(INC, "spgg_test.h"), os.path.join(PKG_DIR, "csrc", "spgg_device.h"),
               os.path.join(PKG_DIR, "csrc", "spgg_mt.h")]
 
 

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "spgg_abi.h"
+#include "spgg_test.h"
 #include "spgg_device.h"
 #include "spgg_mt.h"
 
@@ -2295,8 +2296,8 @@ struct spgg_ctx {
   uint32_t* d_err = nullptr;         // generator error word (SPGG_GEN_ERR_*, sticky per context)
   volatile uint32_t* h_err = nullptr;  // its pinned host copy, refreshed after every chunk
   int gen_upto = 0;                  // iterations whose generation is enqueued
-  std::vector<double> kappa_host;  // the replicas' kappa as last set
-  bool kappa_woke = false;         // a kappa went 0 -> nonzero since the run's iteration 1
+  std::vector<spgg_rep_params> params_host;  // the replicas' parameters as last set
+  bool params_moved = false;  // a replica's parameters changed since the run's iteration 1
   spgg_rep_params* d_params = nullptr;
   int2* d_ring = nullptr;   // ring table (geometry of the tiling)
   int ring_max = 0;
@@ -2335,6 +2336,13 @@ int create_fail(int code, const std::string& msg) {
 int hip_check(spgg_ctx* c, hipError_t e, const char* what) {
   if (e == hipSuccess) return SPGG_OK;
   return fail(c, SPGG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// A tuning knob's value (spgg_abi.h, "Environment knobs"), read only when SPGG_TUNING=1: a stray
+// variable in a user's environment never changes the layout or the schedule of a production run.
+const char* tuning_env(const char* name) {
+  const char* on = getenv("SPGG_TUNING");
+  return on && !strcmp(on, "1") ? getenv(name) : nullptr;
 }
 
 // Below this many workgroups per launch (at the operator's agents per thread)
@@ -2389,14 +2397,14 @@ void choose_mt_chains(spgg_ctx* c) {
       else chains /= 2;
     }
   }
-  if (const char* e = getenv("SPGG_MT_CHAINS")) {
+  if (const char* e = tuning_env("SPGG_MT_CHAINS")) {
     int v = atoi(e), p2 = 1;
     while (p2 < 256 && p2 < v) p2 *= 2;
     chains = W >= 624 ? std::max(1, p2) : 1;  // (a chain's first key block must lie in its window)
   }
-  if (const char* e = getenv("SPGG_MT_PER_CHAIN")) per = std::max(1, std::min(4096, atoi(e)));
+  if (const char* e = tuning_env("SPGG_MT_PER_CHAIN")) per = std::max(1, std::min(4096, atoi(e)));
   if (chains == 1)
-    if (const char* e = getenv("SPGG_MT_CHUNK")) per = std::max(1, std::min(256, atoi(e)));
+    if (const char* e = tuning_env("SPGG_MT_CHUNK")) per = std::max(1, std::min(256, atoi(e)));
   // a chain indexes its words in 32 bits (below 2^31)
   per = (int)std::max(1LL, std::min((long long)per, ((1LL << 31) - (1LL << 16)) / W));
   c->chains = chains;
@@ -2608,7 +2616,7 @@ void launch_gen(const spgg_ctx* c, int t0, int t1, int skip_stopped, hipStream_t
 // (cfg3 MT19937 whole run 71.4 vs 74.1 us/iter, cfg5 36.0 vs 41.3; an idle CU-masked generator
 // stream alone slowed the steps: 59.7 vs 65.6; profiles/r04/generator_stream_modes.txt).
 hipError_t make_stream(hipStream_t* s, bool gen) {
-  const char* e = getenv(gen ? "SPGG_GEN_STREAM_MODE" : "SPGG_STREAM_MODE");
+  const char* e = tuning_env(gen ? "SPGG_GEN_STREAM_MODE" : "SPGG_STREAM_MODE");
   const int mode = e ? atoi(e) : gen ? 0 : 2;
   if (mode == 1 || mode == 4) {  // 1: greatest priority, 4: least (non-blocking)
     int lo = 0, hi = 0;
@@ -2619,7 +2627,7 @@ hipError_t make_stream(hipStream_t* s, bool gen) {
     hipError_t r = hipGetDevice(&dev);
     if (r == hipSuccess) r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (r == hipSuccess && cus > 0) {
-      const char* st = getenv("SPGG_GEN_CU_STRIDE");
+      const char* st = tuning_env("SPGG_GEN_CU_STRIDE");
       const int stride = std::max(2, st ? atoi(st) : 8);
       std::vector<uint32_t> mask((cus + 31) / 32, 0u);
       for (int i = 0; i < cus; ++i)
@@ -2763,7 +2771,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     choose_tile(cfg->L, kBlock * apt_max, &tw4, &th4);
     const long long reps = cfg->batch_reps > 0 ? cfg->batch_reps : cfg->n_rep;
     const long long tiles4 = reps * ((cfg->L + tw4 - 1) / tw4) * ((cfg->L + th4 - 1) / th4);
-    if (const char* e = getenv("SPGG_APT")) {
+    if (const char* e = tuning_env("SPGG_APT")) {
       if (!strcmp(e, "max") || atoi(e) == apt_max) apt = apt_max;
       else if (!strcmp(e, "1")) apt = 1;
       else if (!strcmp(e, "2")) apt = 2;
@@ -2792,7 +2800,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
     c->TW = 20;
     c->TH = 25;
   }
-  if (const char* e = getenv("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
+  if (const char* e = tuning_env("SPGG_TILE")) {  // tuning knob: "<TW>x<TH>"
     int w = 0, h = 0;
     if (sscanf(e, "%dx%d", &w, &h) == 2 && w >= 1 && h >= 1 && w <= std::min(cfg->L, 56) &&
         h <= std::min(cfg->L, 64) && w * h <= kBlock * c->apt) {
@@ -2805,7 +2813,7 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   // history-record stripes: <= kTilesPerStripe workgroups add to one record address per
   // iteration (a single record of an L=1000 replica took 1000 atomics per address: ~12 us)
   int tiles_per_stripe = kTilesPerStripe;
-  if (const char* e = getenv("SPGG_TILES_PER_STRIPE")) tiles_per_stripe = std::max(1, atoi(e));
+  if (const char* e = tuning_env("SPGG_TILES_PER_STRIPE")) tiles_per_stripe = std::max(1, atoi(e));
   while (c->stripes < 32 && (c->tiles_per_rep + c->stripes - 1) / c->stripes > tiles_per_stripe) c->stripes *= 2;
   const int HA = cfg->second_order ? 2 : 1;
   const bool twc = twc_of(*cfg, c->TW, c->TH) > 0;
@@ -2846,12 +2854,13 @@ int spgg_set_params(spgg_ctx* c, const spgg_rep_params* params) {
   }
   rc = hip_check(c, hipMemcpy(c->d_params, params, bytes, hipMemcpyHostToDevice), "hipMemcpy(params)");
   if (rc) return rc;
-  // kappa == 0 replicas keep no pending NI record (md / atd): continuing a run after one of them
-  // turned nonzero would read records that were never written (spgg_step refuses it)
-  if (c->kappa_host.size() == (size_t)c->cfg.n_rep)
-    for (int r = 0; r < c->cfg.n_rep; ++r) c->kappa_woke |= c->kappa_host[r] == 0.0 && params[r].kappa != 0.0;
-  c->kappa_host.resize(c->cfg.n_rep);
-  for (int r = 0; r < c->cfg.n_rep; ++r) c->kappa_host[r] = params[r].kappa;
+  // parameters are fixed for a run: kappa == 0 replicas keep no pending NI record (md / atd), and
+  // the large-batch kernels rebuild iteration t-1's rewards and |alpha*td'| from the parameters
+  // in force at launch t (recomputed record) -- a change between two spgg_step calls of one run
+  // would apply the deferred NI term with other rewards (spgg_step / spgg_flush refuse to go on)
+  if (c->params_host.size() == (size_t)c->cfg.n_rep)
+    c->params_moved |= memcmp(c->params_host.data(), params, bytes) != 0;
+  c->params_host.assign(params, params + c->cfg.n_rep);
   c->params_set = true;
   return SPGG_OK;
 }
@@ -2886,14 +2895,15 @@ static int step_check(spgg_ctx* c, int32_t t0, int32_t n_steps) {
     return fail(c, SPGG_E_ARG, "spgg_step: iteration range outside [1, iterations]");
   if (c->cfg.rng_mode == SPGG_RNG_INJECT && n_steps > 1)
     return fail(c, SPGG_E_ARG, "spgg_step: INJECT mode steps one iteration per call");
-  if (t0 != 1 && c->kappa_woke)
-    return fail(c, SPGG_E_STATE, "spgg_step: a replica's kappa changed from 0 to nonzero mid-run");
+  if (t0 != 1 && c->params_moved)
+    return fail(c, SPGG_E_STATE, "spgg_step: replica parameters changed mid-run (spgg_set_params after "
+                                 "iteration 1: e.g. a kappa woken from 0 has no pending NI record)");
   return SPGG_OK;
 }
 
 // Run setup of a checked spgg_step call: the iteration-1 prologue and the generator's start.
 static int step_begin(spgg_ctx* c, int32_t t0, int32_t n_steps, hipStream_t s) {
-  if (t0 == 1) c->kappa_woke = false;  // a new run
+  if (t0 == 1) c->params_moved = false;  // a new run
   const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
   if (mt) {
     int rc = mt_lazy_init(c);
@@ -2947,23 +2957,33 @@ int spgg_step_groups(spgg_ctx* const* ctxs, void* const* streams, int32_t n_ctx,
     if (ctxs[i]->cfg.rng_mode == SPGG_RNG_INJECT)
       return fail(ctxs[i], SPGG_E_ARG, "spgg_step_groups: INJECT mode steps through spgg_step");
     int rc = step_check(ctxs[i], t0, n_steps);
-    if (rc) return rc;
+    // the fallible part of step_begin (the generator's lazy setup: allocations, the jump
+    // polynomials) runs here too, so that nothing is enqueued on any context unless every one
+    // of them can start; a failure is reported on that context and on ctxs[0], which callers read
+    if (!rc && ctxs[i]->cfg.rng_mode == SPGG_RNG_MT19937) rc = mt_lazy_init(ctxs[i]);
+    if (rc) {
+      if (i > 0) fail(ctxs[0], rc, "spgg_step_groups: context " + std::to_string(i) + ": " + ctxs[i]->err);
+      return rc;
+    }
   }
   for (int i = 0; i < n_ctx; ++i) {
     int rc = step_begin(ctxs[i], t0, n_steps, reinterpret_cast<hipStream_t>(streams[i]));
-    if (rc) return rc;
+    if (rc) return rc;  // (cannot fail: mt_lazy_init above already succeeded)
   }
   for (int t = t0; t < t0 + n_steps; ++t)
     for (int i = 0; i < n_ctx; ++i) step_iter(ctxs[i], t, t0, reinterpret_cast<hipStream_t>(streams[i]));
-  return hip_check(ctxs[0], hipGetLastError(), "spgg_step_groups launch");
+  const int rc = hip_check(ctxs[0], hipGetLastError(), "spgg_step_groups launch");
+  for (int i = 1; i < n_ctx && rc; ++i) ctxs[i]->err = ctxs[0]->err;
+  return rc;
 }
 
 int spgg_flush(spgg_ctx* c, int32_t t_last, void* stream) {
   if (!c) return SPGG_E_ARG;
   if (!c->bound || !c->params_set) return fail(c, SPGG_E_STATE, "spgg_flush before bind/set_params");
   if (t_last < 1 || t_last > c->cfg.iterations) return fail(c, SPGG_E_ARG, "spgg_flush: bad t_last");
-  if (c->kappa_woke)  // the NI term would read a pending record that was never written
-    return fail(c, SPGG_E_STATE, "spgg_flush: a replica's kappa changed from 0 to nonzero mid-run");
+  if (c->params_moved)  // the NI term would read a pending record that was never written
+    return fail(c, SPGG_E_STATE, "spgg_flush: replica parameters changed mid-run (e.g. a kappa woken "
+                                 "from 0 has no pending NI record)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (c->cfg.rng_mode == SPGG_RNG_MT19937 && c->gen_done[0]) {
     // the generator ran ahead: wait for it, then restore each replica's key to the one the

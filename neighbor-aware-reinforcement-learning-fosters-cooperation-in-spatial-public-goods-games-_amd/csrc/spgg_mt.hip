@@ -12,7 +12,6 @@
 #include <cstring>
 #include <map>
 #include <mutex>
-#include <thread>
 #include <vector>
 
 namespace spgg_mt {
@@ -89,7 +88,7 @@ Poly derive_phi() {
   return phi;
 }
 
-// (heap objects never freed: the warm-up thread below may still run at process exit)
+// (heap objects never freed: spgg_create's prefetch thread may still run at process exit)
 const Poly& phi() {
   static const Poly* p = new Poly(derive_phi());
   return *p;
@@ -122,18 +121,10 @@ const std::vector<uint64_t>& red_table() {
   return *T;
 }
 
-// phi (Berlekamp-Massey, ~30 ms) and the reduction table built on a thread of their own when the
-// library loads: a run's first MT19937 launch (spgg_step's jump polynomials) finds them ready
-// instead of paying for them on the host before its first step (the function-local statics make
-// a caller that comes first wait for the same initialisation)
-struct MtHostWarmup {
-  MtHostWarmup() {
-    try {
-      std::thread([] { (void)red_table(); }).detach();
-    } catch (...) {  // no thread: built on first use
-    }
-  }
-} mt_host_warmup;
+// (phi, ~30 ms of Berlekamp-Massey, and the reduction table are built by the first jump_poly
+// call: spgg_create's prefetch thread of an MT19937 context with chains, so no thread starts
+// when the library loads -- a fork() while one held these statics' guards would leave the child
+// blocked on its first jump)
 
 // q (degree <= 2 (kDeg - 1), 2 kPW + 2 words) mod phi, eight coefficients at a time from the top
 void reduce_mod(std::vector<uint64_t>& q) {

@@ -33,6 +33,15 @@ from . import _lib as C
 from .algorithms import canonical_name
 
 SNAPSHOT_ITERS = (1, 10, 100, 1000, 5000, 10000, 20000, 30000, 40000)  # spgg.py:153
+
+
+def tuning_env(name: str, default: Optional[str] = None) -> Optional[str]:
+    """A scheduling / layout knob (SPGG_CACHE_MB, SPGG_CHUNK, SPGG_STREAMS, ...), read only when
+    SPGG_TUNING=1 -- as the library reads its own (spgg_abi.h, "Environment knobs"): a stray
+    variable in a user's environment never changes how a production run is scheduled."""
+    if os.environ.get("SPGG_TUNING") != "1":
+        return default
+    return os.environ.get(name, default)
 PNG_ITERS = set(SNAPSHOT_ITERS) | {5000}                                 # spgg.py:553
 
 
@@ -297,15 +306,15 @@ class BatchEngine:
         # stream each) for `chunk` iterations while the next wave's groups queue
         # behind them on the same streams (groups are independent: results are
         # unchanged, only the order of launches across groups)
-        self.cache_bytes = int(float(os.environ.get("SPGG_CACHE_MB", "240")) * 2**20)
-        self.chunk = max(1, int(os.environ.get("SPGG_CHUNK", "64")))
-        self.enqueue_chunk = int(os.environ.get("SPGG_ENQ_CHUNK", "8"))
+        self.cache_bytes = int(float(tuning_env("SPGG_CACHE_MB", "240")) * 2**20)
+        self.chunk = max(1, int(tuning_env("SPGG_CHUNK", "64")))
+        self.enqueue_chunk = int(tuning_env("SPGG_ENQ_CHUNK", "8"))
         # resident replica groups enqueued iteration by iteration in one call (spgg_step_groups);
         # SPGG_INTERLEAVE=0: one spgg_step call per group and enqueue_chunk iterations
-        self.interleave = os.environ.get("SPGG_INTERLEAVE", "1") != "0"
-        self.skip_dead = os.environ.get("SPGG_SKIP_DEAD", "1") != "0"
-        if streams is None and os.environ.get("SPGG_STREAMS"):
-            streams = int(os.environ["SPGG_STREAMS"]) or None
+        self.interleave = tuning_env("SPGG_INTERLEAVE", "1") != "0"
+        self.skip_dead = tuning_env("SPGG_SKIP_DEAD", "1") != "0"
+        if streams is None and tuning_env("SPGG_STREAMS"):
+            streams = int(tuning_env("SPGG_STREAMS")) or None
         self.waves, self.G, self.resident = plan_groups(
             self.R, self.L, self.state_bytes_per_replica(), self.cache_bytes, streams, single=rng == "inject")
         self._alloc()
@@ -342,7 +351,7 @@ class BatchEngine:
         self.S[0].copy_(torch.from_numpy(S0))
         units = [p.rep_unit() for p in self.reps]
         self.rep_int8 = (all(u is not None for u in units)
-                         and os.environ.get("SPGG_REP_F64", "0") != "1")
+                         and tuning_env("SPGG_REP_F64", "0") != "1")
         self.rep_units = np.array([u if u is not None else 1.0 for u in units])
         self.Rep = torch.zeros((2, R, n), dtype=torch.int8 if self.rep_int8 else f64, device=d)
         # Q updated in place, in state planes per replica (spgg_abi.h; to_state_planes)
@@ -387,7 +396,7 @@ class BatchEngine:
         self._own_streams = []
         if self.G == 1:
             streams = [torch.cuda.current_stream(self.dev)]
-        elif os.environ.get("SPGG_OWN_STREAMS", "1") == "1":
+        elif tuning_env("SPGG_OWN_STREAMS", "1") == "1":
             # streams made by the library (spgg_stream_create, SPGG_STREAM_MODE), not torch's pool:
             # torch's pool streams share HIP's few hardware queues with every earlier user, and
             # two streams on one queue run serialised (cfg3, a second engine in the process:

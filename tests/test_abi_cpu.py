@@ -9,23 +9,29 @@ import pytest
 
 from spgg_amd import _lib
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "spgg_abi.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADER = os.path.join(INCLUDE, "spgg_abi.h")
+TEST_HEADER = os.path.join(INCLUDE, "spgg_test.h")
 
 
-def _declared():
-    src = open(HEADER).read()
+def _declared(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(spgg_\w+)\s*\(", src, flags=re.M))
 
 
 def test_header_declares_the_bound_functions():
+    """The product header declares exactly the product binding; the test hooks live in
+    spgg_test.h alone (never in the product ABI a reference-side binding copies)."""
     assert _declared() == set(_lib.EXPORTED)
+    assert _declared(TEST_HEADER) == set(_lib.TEST_EXPORTED)
+    assert not set(_lib.TEST_EXPORTED) & _declared()
 
 
 @pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
 def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
-    missing = [name for name in sorted(_declared()) if not hasattr(lib, name)]
+    missing = [name for name in sorted(_declared() | _declared(TEST_HEADER)) if not hasattr(lib, name)]
     assert not missing, missing
 
 
@@ -68,6 +74,7 @@ def test_create_failures_report_a_reason(monkeypatch):
     assert rc == _lib.E_ARG and "batch_reps" in msg
     rc, msg = create(algorithm=9)
     assert rc == _lib.E_ARG and "algorithm" in msg
+    monkeypatch.setenv("SPGG_TUNING", "1")
     monkeypatch.setenv("SPGG_APT", "3")
     rc, msg = create()
     assert rc == _lib.E_ARG and "SPGG_APT=3" in msg and "max" in msg
@@ -111,3 +118,26 @@ def test_only_documented_environment_knobs_are_read():
     knobs = header[header.index("Environment knobs"):header.index("int spgg_create")]
     undocumented = sorted(n for n in names if n not in knobs)
     assert not undocumented, undocumented
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspgg_hip.so not built")
+def test_tuning_knobs_need_the_tuning_switch(monkeypatch):
+    """Without SPGG_TUNING=1 the library ignores its tuning knobs: an SPGG_APT or SPGG_TILE
+    left in a user's environment changes nothing (here: a value that would fail spgg_create
+    is not even read, and the tile is the planner's)."""
+    lib = _lib.load()
+    base = dict(device=0, n_rep=2, L=200, second_order=0, state_mode=_lib.STATE_REPUTATION,
+                rng_mode=_lib.RNG_PHILOX, iterations=10, rep_int8=1, algorithm=_lib.ALG_QLEARNING)
+    monkeypatch.delenv("SPGG_TUNING", raising=False)
+    monkeypatch.setenv("SPGG_APT", "3")
+    monkeypatch.setenv("SPGG_TILE", "16x16")
+    ctx = ctypes.c_void_p()
+    rc = lib.spgg_create(ctypes.byref(ctx), _lib.Config(**base))
+    if rc == _lib.E_HIP:   # no device in this container: creation stops at hipSetDevice
+        assert "SPGG_APT" not in lib.spgg_last_error(None).decode()
+        return
+    assert rc == _lib.OK
+    tw, th = ctypes.c_int32(), ctypes.c_int32()
+    assert lib.spgg_tile_shape(ctx, ctypes.byref(tw), ctypes.byref(th)) == _lib.OK
+    assert (tw.value, th.value) != (16, 16)
+    lib.spgg_destroy(ctx)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Tilings of the latency-bound configs: agents per thread (SPGG_APT 1 / 2 / max) x replica groups,
 # Philox windows (no MT, no whole run), then eager vs hipGraph replay.  Output: gpurun_out/apt/.
+export SPGG_TUNING=1   # the knobs below are read only with the tuning switch
 cd "$GRAFT_REPO_ROOT"; O="$GRAFT_REPO_ROOT/gpurun_out/apt"; mkdir -p "$O"; export TMPDIR=/tmp
 : > $O/lines.txt
 run() {  # name apt streams

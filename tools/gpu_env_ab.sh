@@ -2,6 +2,7 @@
 # A/B of run-time settings (environment assignments) on the bench's default window and steady
 # window, ONE fresh process per setting and round.  usage: gpu_env_ab.sh ROUNDS "VAR=a" "VAR=b" ...
 # ("-" = no assignment).  Output: gpurun_out/envab/ab.txt (one line per run) + a summary.
+export SPGG_TUNING=1   # the knobs below are read only with the tuning switch
 cd "$GRAFT_REPO_ROOT"; O="$GRAFT_REPO_ROOT/gpurun_out/envab"; mkdir -p "$O"; export TMPDIR=/tmp
 R=$1; shift
 for r in $(seq $R); do

@@ -1,3 +1,4 @@
+export SPGG_TUNING=1   # the knobs below are read only with the tuning switch
 cd "$GRAFT_REPO_ROOT"; O="$GRAFT_REPO_ROOT/gpurun_out/fr"; mkdir -p "$O"
 for r in 1 2; do
   for E in SPGG_INTERLEAVE=1 SPGG_INTERLEAVE=0; do

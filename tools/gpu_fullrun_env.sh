@@ -1,6 +1,7 @@
 #!/bin/bash
 # Whole-run timing (tools/fullrun_probe.py, Philox) of run-time settings, one fresh process each.
 # usage: gpu_fullrun_env.sh ROUNDS CONFIG ITERS "VAR=a" ... ("-" = none).  Output: gpurun_out/fre/fr.txt
+export SPGG_TUNING=1   # the knobs below are read only with the tuning switch
 cd "$GRAFT_REPO_ROOT"; O="$GRAFT_REPO_ROOT/gpurun_out/fre"; mkdir -p "$O"
 R=$1; C=$2; N=$3; shift 3
 for r in $(seq $R); do

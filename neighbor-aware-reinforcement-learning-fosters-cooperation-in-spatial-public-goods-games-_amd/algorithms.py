@@ -2,10 +2,20 @@
 
 The classes keep the reference's constructor signature, attributes, eps
 schedule (`decay_epsilon`, algorithms.py:40-42) and the `create_algorithm`
-factory with its ValueError.  Their per-lattice `select_action` /
-`update_q_table` arithmetic is fused into the HIP step (libspgg_hip.so) and
-driven by `SPGG.run` / `BatchEngine`; calling those two methods on their own
-raises, because this package has no NumPy execution path by design.
+factory with its ValueError.
+
+Two execution paths:
+  * `SPGG.run` / `BatchEngine` never call these methods: the per-lattice
+    `select_action` / `update_q_table` arithmetic of the four operators is fused into
+    the HIP step (libspgg_hip.so, one template instance per operator);
+  * a caller that uses the operator interface directly (the reference's own
+    `algorithm.select_action(...)` / `.update_q_table(...)` calls, spgg.py:410-441)
+    gets the same results on the host: the methods below are NumPy restatements that
+    consume the global `np.random` stream exactly as the reference's do (rand, then
+    randint per select; Double-Q's rand < 0.5 table choice), so a mixed host / device
+    caller keeps the reference's stream.  Pinned bit for bit by
+    tests/golden/operator_calls.npz (made by importing the reference,
+    tests/golden/make_operator_golden.py; tests/test_operator_host_cpu.py).
 
 The plug-in point (`SPGG(algorithm=<RLAlgorithm instance>)`, spgg.py:111-118):
 `operator_kind` accepts these four classes, the reference's own four (an
@@ -13,10 +23,6 @@ instance built from src/model/algorithms.py drops in) and subclasses that only
 add state; anything that redefines the operator's methods is refused with a
 ValueError naming the class, so custom arithmetic can never silently run as the
 built-in operator.
-
-GPU coverage: all four operators -- QLearning (algorithms.py:96-133), SARSA
-(:136-178), ExpectedSARSA (:181-234), DoubleQLearning (:237-341) -- each a
-template instance of the step kernel (spgg_kernels.hip, SPGG_ALG_*).
 """
 from __future__ import annotations
 
@@ -44,29 +50,87 @@ class RLAlgorithm(ABC):
         self.epsilon = max(self.epsilon * self.epsilon_decay, self.epsilon_min)
 
     def select_action(self, q_table, states, L, **kwargs):
-        raise NotImplementedError(
-            f"{type(self).__name__}.select_action is fused into the HIP step; drive it "
-            "through SPGG.run() or BatchEngine")
+        """eps-greedy actions over the (L, L) lattice (algorithms.py:102-110, the same in all
+        four operators): ONE rand(L, L) then ONE randint(0, 2, (L, L)) from the global stream;
+        greedy = first argmax of the agent's row Q[i, j, s_ij, :] (ties -> action 0)."""
+        return _eps_greedy(q_table, states, L, self.epsilon)
 
     def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
-        raise NotImplementedError(
-            f"{type(self).__name__}.update_q_table is fused into the HIP step; drive it "
-            "through SPGG.run() or BatchEngine")
+        """TD update of entry (s, a) of every agent, in place; returns the table."""
+        raise NotImplementedError("RLAlgorithm.update_q_table is abstract (algorithms.py:44-70)")
+
+    def _td(self, q_table, old_states, actions, rewards, target):
+        """Q[s, a] <- Q[s, a] + alpha * ((r + gamma * target) - Q[s, a]) in place: the
+        reference's evaluation order (algorithms.py:128-131)."""
+        q = _entries(q_table, old_states, actions)
+        td = rewards + self.gamma * target - q
+        _put_entries(q_table, old_states, actions, q + self.alpha * td)
+        return q_table
+
+
+def _rows(q_table, states):
+    """Q[i, j, states[i, j], :] of every agent, shape (L, L, actions)."""
+    s = np.asarray(states)
+    return np.take_along_axis(q_table, s[:, :, None, None], axis=2)[:, :, 0, :]
+
+
+def _entries(q_table, states, actions):
+    """Q[i, j, states[i, j], actions[i, j]], shape (L, L)."""
+    row = _rows(q_table, states)
+    return np.take_along_axis(row, np.asarray(actions)[:, :, None], axis=2)[:, :, 0]
+
+
+def _put_entries(q_table, states, actions, values):
+    """Q[i, j, states[i, j], actions[i, j]] = values (each agent's entry written once)."""
+    L0, L1 = q_table.shape[:2]
+    ii, jj = np.meshgrid(np.arange(L0), np.arange(L1), indexing="ij")
+    q_table[ii, jj, np.asarray(states), np.asarray(actions)] = values
+
+
+def _eps_greedy(q_table, states, L, epsilon):
+    """algorithms.py:105-109: explore = rand < eps (drawn first), greedy = argmax of the row
+    (first maximum), random action = randint(0, 2) (drawn second)."""
+    explore = np.random.rand(L, L) < epsilon
+    greedy = np.argmax(_rows(q_table, states), axis=2)
+    random_action = np.random.randint(0, 2, size=(L, L))
+    return np.where(explore, random_action, greedy)
 
 
 class QLearning(RLAlgorithm):
     """Off-policy TD with max over next-state actions (algorithms.py:96-133)."""
     kind = "qlearning"
 
+    def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
+        """target = max_a' Q[s', a'] (algorithms.py:124-131)."""
+        return self._td(q_table, old_states, actions, rewards, _rows(q_table, new_states).max(axis=2))
+
 
 class SARSA(RLAlgorithm):
     """On-policy TD (algorithms.py:136-178)."""
     kind = "sarsa"
 
+    def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
+        """target = Q[s', a'] of the next actions the caller passes (algorithms.py:159-176)."""
+        if "next_actions" not in kwargs:
+            raise ValueError("SARSA requires 'next_actions' parameter")
+        target = _entries(q_table, new_states, kwargs["next_actions"])
+        return self._td(q_table, old_states, actions, rewards, target)
+
 
 class ExpectedSARSA(RLAlgorithm):
     """Expected-value TD under the eps-greedy policy (algorithms.py:181-234)."""
     kind = "expected_sarsa"
+
+    def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
+        """target = sum_a' pi(a'|s') Q[s', a'] with pi eps-greedy: eps / A everywhere plus
+        (1 - eps) on the first argmax, summed over a' in order (algorithms.py:212-229)."""
+        nxt = _rows(q_table, new_states)
+        A = q_table.shape[3]
+        other = self.epsilon / A
+        probs = np.full(nxt.shape, other)
+        greedy = np.argmax(nxt, axis=2)
+        np.put_along_axis(probs, greedy[:, :, None], (1 - self.epsilon) + other, axis=2)
+        return self._td(q_table, old_states, actions, rewards, np.sum(probs * nxt, axis=2))
 
 
 class DoubleQLearning(RLAlgorithm):
@@ -88,6 +152,30 @@ class DoubleQLearning(RLAlgorithm):
         if self.q_table_1 is None or self.q_table_2 is None:
             raise ValueError("Q-tables not initialized. Call initialize_q_tables first.")
         return (self.q_table_1 + self.q_table_2) / 2
+
+    def select_action(self, q_table, states, L, **kwargs):
+        """eps-greedy on the mean table; before initialize_q_tables on the table passed in
+        (algorithms.py:268-290)."""
+        if self.q_table_1 is None or self.q_table_2 is None:
+            return _eps_greedy(q_table, states, L, self.epsilon)
+        return _eps_greedy(self.get_combined_q_table(), states, L, self.epsilon)
+
+    def update_q_table(self, q_table, old_states, actions, rewards, new_states, **kwargs):
+        """Per agent one rand(L, L) < 0.5 picks the table updated (q_table_1 where true),
+        evaluated at the OTHER table's greedy next action; returns the mean table
+        (algorithms.py:292-341; the q_table argument is not read)."""
+        if self.q_table_1 is None or self.q_table_2 is None:
+            raise ValueError("Q-tables not initialized. Call initialize_q_tables first.")
+        L = self.q_table_1.shape[0]
+        first = np.random.rand(L, L) < 0.5
+        n1, n2 = _rows(self.q_table_1, new_states), _rows(self.q_table_2, new_states)
+        # Q1's target: Q2 at Q2's argmax; Q2's target: Q1 at Q1's argmax (= each row's max)
+        t1, t2 = n2.max(axis=2), n1.max(axis=2)
+        for tab, target, mask in ((self.q_table_1, t1, first), (self.q_table_2, t2, ~first)):
+            q = _entries(tab, old_states, actions)
+            new = q + self.alpha * (rewards + self.gamma * target - q)
+            _put_entries(tab, old_states, actions, np.where(mask, new, q))
+        return self.get_combined_q_table()
 
 
 _ALIASES = {"qlearning": "qlearning", "q-learning": "qlearning", "sarsa": "sarsa",

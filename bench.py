@@ -321,6 +321,7 @@ def main(argv=None):
         if dist:
             dist.barrier()
         wall = time.perf_counter() - t0
+        eng.check_status()   # a generator or persistent-barrier failure raises (no silent number)
         dev_ms = max(a_.elapsed_time(b_) for a_ in ev0 for b_ in ev1)
         stop = eng.stop_iter.cpu().numpy()
         # executed iterations in the timed window [W+1, W+K] per replica
@@ -343,7 +344,7 @@ def main(argv=None):
             agent_steps_all, wall_max = agent_steps, wall
         out = dict(agent_steps=agent_steps, agent_steps_all=agent_steps_all, wall=wall, wall_max=wall_max,
                    dev_ms=dev_ms, coop=coop, trace=trace, mt_layout=mt_layout, resident=eng.resident,
-                   groups=eng.G, waves=eng.waves)
+                   groups=eng.G, waves=eng.waves, persistent=eng.persistent)
         eng.close()   # before the next engine, the full run and the CPU baseline's worker processes
         return out
 
@@ -367,6 +368,12 @@ def main(argv=None):
     achieved = ALGO_BYTES_PER_AGENT_STEP * step_agents / per_step_dev_s / 1e9
     achieved_wall = ALGO_BYTES_PER_AGENT_STEP * agent_steps / wall / 1e9
     resident, groups, waves = main_w["resident"], main_w["groups"], main_w["waves"]
+    persistent = main_w["persistent"]
+    # the step kernel the window ran: one launch per iteration and replica group, or (the whole
+    # batch resident at once) one persistent launch per group for the K iterations
+    step_kernel = (f"spgg_persist_kernel, {resident} concurrent launch(es) covering the {K} timed iterations "
+                   f"(Q rows held in registers, a per-replica barrier between iterations)" if persistent else
+                   f"spgg_step_kernel, {resident} concurrent launches per iteration (one per replica group/stream)")
     # the drop-in SPGG.run / sweep path: the device MT19937 stream, bit-identical to the reference
     mt_w = window("mt19937") if args.rng == "philox" and not args.no_mt else None
     steady = None
@@ -390,7 +397,7 @@ def main(argv=None):
             "config": {"workload": desc, "window": f"iterations {W + 1}-{W + K}", "L": L, "replicas_per_gpu": len(reps),
                        "agents_per_gpu": n_agents, "second_order": M2, "state": state,
                        "rng": args.rng, "seeds_rank0": seed_range(reps), "seeds_all_ranks": f"0-{int(gathered_seed_max)}",
-                       "streams_per_gpu": resident, "replica_groups": groups,
+                       "streams_per_gpu": resident, "replica_groups": groups, "persistent": persistent,
                        "cache_waves": waves, "mt_chains": mt_layout,
                        "parallelism": f"replicas sharded over {world} GPU(s)"},
             "gather": {"replicas": int(gathered_rows.shape[0] * gathered_rows.shape[1]),
@@ -406,12 +413,10 @@ def main(argv=None):
                                          + (os.path.relpath(tfile, ROOT) if tfile else "no PMC traffic file"),
                          "traffic_gbs": (traffic / per_step_dev_s / 1e9) if traffic else None,
                          "algorithmic_bytes_per_agent_step": ALGO_BYTES_PER_AGENT_STEP,
-                         "kernel": (f"spgg_step_kernel, {resident} concurrent launches per iteration "
-                                    f"(one per replica group/stream)" if args.rng == "philox" else
-                                    f"spgg_step_kernel ({resident} concurrent launches per iteration) + "
-                                    f"spgg_mt_gen_kernel (one launch per chunk of {mt_layout['chains_per_replica']} "
-                                    f"chains x {mt_layout['iterations_per_chain']} iterations per group) + "
-                                    f"spgg_mt_jump_kernel, on their own stream"),
+                         "kernel": (step_kernel if args.rng == "philox" else
+                                    f"{step_kernel} + spgg_mt_gen_kernel (one launch per chunk of "
+                                    f"{mt_layout['chains_per_replica']} chains x {mt_layout['iterations_per_chain']} "
+                                    f"iterations per group) + spgg_mt_jump_kernel, on their own stream"),
                          "device_ms_per_step": per_step_dev_s * 1e3},
         }
         T_full = FULL_RUN_ITERS.get(args.config, 0) if args.full_run < 0 else args.full_run

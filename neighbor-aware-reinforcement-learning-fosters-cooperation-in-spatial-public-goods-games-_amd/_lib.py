@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libspgg_hip.so")
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 OK, E_ARG, E_STATE, E_HIP = 0, -1, -2, -3
 GEN_ERR_SPIN = 1
 STATE_REPUTATION, STATE_ACTION = 0, 1
@@ -37,7 +37,7 @@ EXPORTED = ("spgg_abi_version", "spgg_build_id", "spgg_last_error", "spgg_create
             "spgg_destroy", "spgg_draw_planes", "spgg_pub_doubles", "spgg_stat_stripes",
             "spgg_history_finalize", "spgg_draw_layout", "spgg_set_draw_stream", "spgg_draw_range",
             "spgg_mt_chains", "spgg_mt_jump_poly", "spgg_stream_create", "spgg_stream_destroy",
-            "spgg_status")
+            "spgg_status", "spgg_persistent")
 # test-only entry points (include/spgg_test.h): exported by the library, not part of the product ABI
 TEST_EXPORTED = ("spgg_test_set_error",)
 
@@ -117,6 +117,8 @@ def load(path: str | None = None):
         lib.spgg_payoff.argtypes = [vp, i32, vp, vp]
         lib.spgg_tile_shape.restype = ctypes.c_int
         lib.spgg_tile_shape.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        lib.spgg_persistent.restype = ctypes.c_int
+        lib.spgg_persistent.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         lib.spgg_destroy.restype = ctypes.c_int
         lib.spgg_destroy.argtypes = [vp]
         lib.spgg_draw_planes.restype = ctypes.c_int

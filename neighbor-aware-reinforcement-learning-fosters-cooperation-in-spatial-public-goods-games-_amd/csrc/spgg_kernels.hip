@@ -110,9 +110,37 @@ struct LaunchCfg {
   size_t lds_bytes;
 };
 
-// Enqueue one step-kernel launch of operator ALG (defined in that operator's TU).
+// A persistent launch (spgg_persist_kernel): iterations t0 .. t_end in one launch.  The buffers
+// a neighbouring workgroup reads are ping-ponged by iteration parity as between launches (S, R,
+// border records), so the kernel picks them per iteration from both halves; the draw record of
+// iteration t is ring slot (t-1) % draw_slots.  Between two iterations each workgroup arrives at
+// its replica's counters (one per shard: tile % shards) and waits for every tile of the replica:
+// counter j reaches tiles_in_shard(j) x (base + k) after the k-th barrier of this launch (base:
+// the barriers this run's earlier persistent launches completed; the counters are zeroed at the
+// run's first one).
+struct PersistArgs {
+  uint8_t* S[2];
+  void* R[2];
+  double* pub[2];
+  const uint32_t* draws0;  // draw ring slot 0 (INJECT / MT19937; null for Philox)
+  long long draw_stride;   // u32 words between ring slots
+  int draw_slots;
+  int t_end;               // last iteration of the launch
+  uint32_t* bar;           // arrival counters [n_rep][shards][kBarWords] (one 64-byte line each)
+  int shards;
+  uint32_t base;
+  uint32_t* err;           // error word: SPGG_STEP_ERR_BARRIER when a wait ran out of its bound
+};
+constexpr int kBarWords = 16;
+
+// Enqueue one step-kernel launch of operator ALG (defined in that operator's TU): iteration t
+// (pa == nullptr), or the persistent launch of iterations t .. pa->t_end.
 template <int ALG>
-void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s);
+void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s,
+                const PersistArgs* pa = nullptr);
+// Workgroups of the persistent instance for lc that one CU holds at once (0: no such instance).
+template <int ALG>
+int persist_blocks_per_cu(const LaunchCfg& lc);
 
 // Agents per thread of operator ALG's kernel: tiles of up to 1024 agents
 // (Double-Q, holding two tables in registers: 512).
@@ -234,6 +262,20 @@ __device__ __forceinline__ T* at(T* base, uint32_t i) {
   return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + (size_t)(i * (uint32_t)sizeof(T)));
 }
 
+// A load / store of element p, plain or (SC1: inside a persistent launch, for bytes another
+// workgroup reads) write-through / past the CU's L1 -- relaxed agent-scope atomics, lowered to
+// global_load / global_store ... sc1 (the hand-off rules: replica_barrier below).
+template <bool SC1, typename T>
+__device__ __forceinline__ T hload(const T* p) {
+  if constexpr (SC1) return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool SC1, typename T>
+__device__ __forceinline__ void hstore(T* p, T v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 // Compact reputation: when rep_gain_C, delta_R_D, R_min, R_max are multiples
 // of a dyadic unit u with |R/u| <= 127 (host-checked), every R the reference
 // can produce is k*u exactly, its f64 sums and clip are exact, and
@@ -298,10 +340,12 @@ __device__ __forceinline__ int pending_entry(uint8_t b) { return ((b >> 1) & 1) 
 
 // Wave sums of K values into red[wave*64 + base + k] (f64, or packed integer
 // counters stored as exact doubles).
+// (tid: the thread's index -- threadIdx.x, passed in so that a persistent launch's loop can make it
+// opaque per iteration: derived lane values are then recomputed instead of held across iterations)
 template <int K, typename T>
-__device__ __forceinline__ void wave_partials(T (&v)[K], double* red, int base) {
-  transpose_level<K, 32, K, T>(v, threadIdx.x & 63);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ void wave_partials(T (&v)[K], double* red, int base, int tid) {
+  transpose_level<K, 32, K, T>(v, tid & 63);
+  const int lane = tid & 63, wave = tid >> 6;
   constexpr int per = 64 / K;
   if ((lane & (per - 1)) == 0) red[wave * 64 + base + lane / per] = (double)v[0];
 }
@@ -365,10 +409,11 @@ __device__ __forceinline__ void stage_region(T* dst, int pitch, const T* src, in
 template <int J, int W, typename T>
 struct RowWindow {
   StageReg<T> buf[J];
-  __device__ __forceinline__ void load(const T* src, int h, int y0, int x0, int L) {
+  template <bool SC1 = false>
+  __device__ __forceinline__ void load(const T* src, int h, int y0, int x0, int L, int tid) {
     static_assert(W <= 64, "one row per wave instruction");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int gx = x0 + (lane < W ? lane : W - 1);
     gx += gx < 0 ? L : 0;
     gx -= gx >= L ? L : 0;
@@ -378,13 +423,13 @@ struct RowWindow {
       int gy = y0 + row;
       gy += gy < 0 ? L : 0;
       gy -= gy >= L ? L : 0;
-      buf[j] = *at(src, (uint32_t)(gy * L + gx));
+      buf[j] = hload<SC1>(at(src, (uint32_t)(gy * L + gx)));
     }
   }
   template <int PITCH>
-  __device__ __forceinline__ void store(T* dst, int h, uint8_t* dbit) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __device__ __forceinline__ void store(T* dst, int h, uint8_t* dbit, int tid) {
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool in_row = lane < W;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -418,20 +463,20 @@ template <int J, int DW>
 struct DwordWindow {
   static constexpr int RPP = kBlock / DW;
   uint32_t buf[J];
-  __device__ __forceinline__ void load(const void* plane, int h, int y0, int xb, int L) {
+  template <bool SC1 = false>
+  __device__ __forceinline__ void load(const void* plane, int h, int y0, int xb, int L, int tid) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(plane);
-    const int tid = threadIdx.x, Ld = L >> 2;
+    const int Ld = L >> 2;
     const int r0 = tid / DW, col = tid - (tid / DW) * DW;  // idle threads (r0 >= RPP) load clamped rows
     const uint32_t gx = wrap_once((xb >> 2) + col, Ld);
 #pragma unroll
     for (int j = 0; j < J; ++j) {  // unconditional loads (rows clamped)
       const uint32_t gy = wrap_once(y0 + min(r0 + j * RPP, h - 1), L);
-      buf[j] = *at(src, __umul24(gy, (uint32_t)Ld) + gx);  // gy, Ld < 2^24
+      buf[j] = hload<SC1>(at(src, __umul24(gy, (uint32_t)Ld) + gx));  // gy, Ld < 2^24
     }
   }
   // dst (pitch bytes, a multiple of 4): the window's dwords; dbit: bit0 of each byte.
-  __device__ __forceinline__ void store(uint8_t* dst, int pitch, int h, uint8_t* dbit) {
-    const int tid = threadIdx.x;
+  __device__ __forceinline__ void store(uint8_t* dst, int pitch, int h, uint8_t* dbit, int tid) {
     const int r0 = tid / DW, col = tid - (tid / DW) * DW;
     const int o0 = r0 * pitch + col * 4;
 #pragma unroll
@@ -450,9 +495,9 @@ struct DwordWindow {
 // (y - 1, x - 1) = defector bits of S-window cells (y+1, x+1) and its four
 // neighbours.  One wave row per region row; lanes past the row width compute
 // unused cells (the D plane carries read slack).
-__device__ __forceinline__ void build_plus_counts(uint8_t* pc, const uint8_t* d, int sw, int rows) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void build_plus_counts(uint8_t* pc, const uint8_t* d, int sw, int rows, int tid) {
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int y = wave; y < rows; y += kWaves) {
     const uint8_t* p = d + y * sw + lane;
     const int cnt = p[1] + p[sw] + p[sw + 1] + p[sw + 2] + p[2 * sw + 1];
@@ -468,10 +513,10 @@ __device__ __forceinline__ void build_plus_counts(uint8_t* pc, const uint8_t* d,
 // bytes.  DWPR = dwords per plane row (>= the region width + 2, / 4).
 template <int DWPR>
 __device__ __forceinline__ void build_plus_counts_dw(uint8_t* pc, const uint8_t* dplane, int sw, int rows,
-                                                     int soff) {
+                                                     int soff, int tid) {
   const uint32_t s0 = 8u * soff, s1 = s0 + 8u, s2 = s0 + 16u;
   const int swd = sw >> 2;
-  for (int task = threadIdx.x; task < rows * DWPR; task += kBlock) {
+  for (int task = tid; task < rows * DWPR; task += kBlock) {
     const int y = task / DWPR, xd = task - (task / DWPR) * DWPR;
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(dplane) + y * swd + xd;
     const uint32_t a0 = r0[0], a1 = r0[1];                    // row y    (the cell above)
@@ -487,9 +532,9 @@ __device__ __forceinline__ void build_plus_counts_dw(uint8_t* pc, const uint8_t*
 // The plus-count plane of the PREVIOUS strategies S_{t-1}: bit 3 of every S_t byte (the
 // strategy its owner started iteration t-1 with), from the staged S window itself -- the
 // payoffs of iteration t-1 recomputed for the pending NI record (recomputed_record).
-__device__ __forceinline__ void build_plus_counts_prev(uint8_t* pc, const uint8_t* s, int sw, int rows) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void build_plus_counts_prev(uint8_t* pc, const uint8_t* s, int sw, int rows, int tid) {
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int y = wave; y < rows; y += kWaves) {
     const uint8_t* p = s + y * sw + lane;
     const int cnt = ((p[1] >> 3) & 1) + ((p[sw] >> 3) & 1) + ((p[sw + 1] >> 3) & 1) + ((p[sw + 2] >> 3) & 1) +
@@ -499,11 +544,11 @@ __device__ __forceinline__ void build_plus_counts_prev(uint8_t* pc, const uint8_
 }
 template <int DWPR>
 __device__ __forceinline__ void build_plus_counts_prev_dw(uint8_t* pc, const uint8_t* splane, int sw, int rows,
-                                                          int soff) {
+                                                          int soff, int tid) {
   const uint32_t s0 = 8u * soff, s1 = s0 + 8u, s2 = s0 + 16u;
   const int swd = sw >> 2;
   constexpr uint32_t kB3 = 0x01010101u;
-  for (int task = threadIdx.x; task < rows * DWPR; task += kBlock) {
+  for (int task = tid; task < rows * DWPR; task += kBlock) {
     const int y = task / DWPR, xd = task - (task / DWPR) * DWPR;
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(splane) + y * swd + xd;
     const uint32_t a0 = (r0[0] >> 3) & kB3, a1 = (r0[1] >> 3) & kB3;
@@ -819,6 +864,81 @@ __device__ __forceinline__ float prev_diag_td(const double (&q)[4], const double
   }
 }
 
+// ---- persistent launches: hand-offs between the workgroups of one replica ----------------
+// Inside one persistent launch every byte that another workgroup reads (the S / R halo
+// windows, the border records, the history record's NCOOP / lattice max) is stored
+// write-through and loaded past the CU's vector L1: relaxed agent-scope atomic stores and loads,
+// which gfx950 lowers to global_store / global_load ... sc1.  With each storing wave's
+// vmcnt(0), one arrival per workgroup after its barrier, an sc1 poll and a workgroup barrier
+// before the loads, no acquire / release fence is needed (MI355X_MICROARCH.md, inter-workgroup
+// visibility: an agent-scope acquire costs ~6.5 us per phase at 4 workgroups per CU).  The
+// per-launch form (SC1 = false) keeps plain accesses: a launch boundary orders them.
+// (hload / hstore: the accessors above, sc1 in persistent launches)
+
+// Sum / max of one f64 per lane over the wave, in every lane (permlane swaps + DPP, no LDS).
+__device__ __forceinline__ double wave_sum(double v) {
+  {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  v += partner<8>(v);
+  v += partner<4>(v);
+  v += partner<2>(v);
+  v += partner<1>(v);
+  return v;
+}
+
+// Bound of a persistent launch's wait for its replica's other tiles, in polls (each an sc1
+// load round trip, >= ~0.5 us, plus s_sleep): >= ~1 s.  Every tile of a persistent launch is
+// co-resident (the host checks the batch against the instance's occupancy), so a wait that
+// runs out means a tile never arrived: the launch records SPGG_STEP_ERR_BARRIER and stops
+// instead of hanging the GPU.
+constexpr uint32_t kBarrierPolls = 1u << 21;
+
+// The replica barrier between two iterations of a persistent launch: every tile of replica rep
+// has finished its k-th iteration of the launch (its S / R / border-record stores and history
+// atomics drained).  Returns false when this wait, or another workgroup's, ran out of its bound.
+__device__ __forceinline__ bool replica_barrier(const spgg_impl::PersistArgs& pa, int rep, int tile,
+                                                int tiles_per_rep, uint32_t k) {
+  __shared__ int bar_ok;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores and atomics have landed
+  __syncthreads();                                  // ... and every other wave's
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x, S = pa.shards;
+    uint32_t* ctr = pa.bar + (size_t)rep * S * spgg_impl::kBarWords;
+    if (lane == 0)
+      __hip_atomic_fetch_add(ctr + (tile % S) * spgg_impl::kBarWords, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    // lane j < S polls shard j (the others repeat shard 0): one load instruction per poll
+    const int j = lane < S ? lane : 0;
+    const uint32_t want = (uint32_t)((tiles_per_rep - j + S - 1) / S) * (pa.base + k);
+    bool ok = false;
+    for (uint32_t poll = 0; poll < kBarrierPolls; ++poll) {
+      const uint32_t have = __hip_atomic_load(ctr + j * spgg_impl::kBarWords, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t err = __hip_atomic_load(pa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_readfirstlane(err) != 0) break;
+      if (__all((int32_t)(have - want) >= 0)) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok && lane == 0) atomicOr(pa.err, (uint32_t)SPGG_STEP_ERR_BARRIER);
+    if (lane == 0) bar_ok = ok ? 1 : 0;
+  }
+  __syncthreads();
+  return bar_ok != 0;
+}
+
 // ONE launch = iteration t of every replica (or, fin_only, the final deferred
 // NI term).  TWC > 0: compile-time tile width, every tile full width (host:
 // L % TWC == 0), so LDS pitches and region divisions are immediates.
@@ -866,9 +986,20 @@ constexpr int min_waves(bool m2, int rng, int twc, int alg) {
 #endif
 }
 
-template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
-__global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_step_kernel(TileArgs a, int t,
-                                                                                         int fin_only) {
+//
+// PERSIST (spgg_persist_kernel): the launch steps iterations t0 .. pa.t_end of replicas whose
+// tiles are all co-resident, each thread keeping its agents' Q rows (and, where the kernel
+// stores it, the pending NI record) in registers from one iteration to the next: they are
+// loaded at the launch's first iteration and stored after its last (or at the absorbing
+// iteration), so an iteration moves only the halo windows, border records and outputs.
+// Between two iterations replica_barrier stands in for the launch boundary (the lattice max
+// and NCOOP of the replica's history record, spgg.py:405,488, and the neighbours' S / R /
+// border records); those hand-offs are sc1 (hload / hstore).  Every workgroup of a replica takes the
+// same absorbing decision at the same iteration (NCOOP), so none waits for a stopped tile.
+template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG, bool PERSIST>
+__device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, const int fin_only,
+                                          const spgg_impl::PersistArgs& pa) {
+  static_assert(!PERSIST || TWC > 0, "persistent launches use the compile-time-width kernels");
   using RT = RStore<RQ>;
   constexpr int HA = M2 ? 2 : 1;  // neighbour radius of the NI / action ring
   constexpr int HS = HA + 2;      // S halo: payoffs over tile + HA
@@ -885,30 +1016,30 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
   // dispatch), so give them consecutive tiles of one replica (shared halos).
-  const int total = a.n_rep * a.tiles_per_rep;
+  const int total = a0.n_rep * a0.tiles_per_rep;
   const int per_xcd = (total + 7) / 8;
   const int logical = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (logical >= total) return;
   if (SPGG_ABLATE & 64) return;
-  const int rep = logical / a.tiles_per_rep;
-  const int tile = logical - rep * a.tiles_per_rep;
+  const int rep = logical / a0.tiles_per_rep;
+  const int tile = logical - rep * a0.tiles_per_rep;
 #if SPGG_STAMPS
   // the workgroup's stamp slot: the batch-wide replica id (stream_id) and tile, so the launches of
   // every replica group (stream) of a batch stamp disjoint slots
-  const int stamp_id = (int)a.params[rep].stream_id * a.tiles_per_rep + tile;
+  const int stamp_id = (int)a0.params[rep].stream_id * a0.tiles_per_rep + tile;
 #endif
 
-  const int L = a.L, n = a.n;
+  const int L = a0.L, n = a0.n;
   const bool tiny = TWC ? false : L < 8;  // TWC => L % TWC == 0
-  const int tyi = tile / a.tiles_x, txi = tile - (tile / a.tiles_x) * a.tiles_x;
-  const int y0 = tyi * a.TH, x0 = txi * a.TW;
-  const int th = min(a.TH, L - y0), tw = TWC ? TWC : min(a.TW, L - x0);
+  const int tyi = tile / a0.tiles_x, txi = tile - (tile / a0.tiles_x) * a0.tiles_x;
+  const int y0 = tyi * a0.TH, x0 = txi * a0.TW;
+  const int th = min(a0.TH, L - y0), tw = TWC ? TWC : min(a0.TW, L - x0);
   // LDS pitches from the full tile width (constants when TWC > 0); edge tiles
   // use the top-left part of each region
   // draw bits staged through LDS (one load round trip with the windows) instead of a record
   // load per agent at the point of use (MT19937 steps 8 us slower than Philox before this)
   constexpr bool DSTAGE = RNG != SPGG_RNG_PHILOX && TWC > 0;
-  const LdsLayout ly = TWC ? lds_layout(TWC, a.TH, HS, HA, (int)sizeof(RT), true, DSTAGE)
+  const LdsLayout ly = TWC ? lds_layout(TWC, a0.TH, HS, HA, (int)sizeof(RT), true, DSTAGE)
                            : lds_layout(tw, th, HS, HA, (int)sizeof(RT));
   double* tab = reinterpret_cast<double*>(smem);
   double* red = tab + 12;
@@ -928,16 +1059,55 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   uint2* sDP = reinterpret_cast<uint2*>(smem + ly.off_DP);         // [row][half] (plane 0, plane 1)
   // this replica's arrays: scalar bases, 32-bit element offsets (at())
   const size_t rb = (size_t)rep * n;
-  double* Qr = a.Q + rb * QW;
-  double* mdr = a.md + rb;
-  float* atdr = a.atd + rb;
+  double* Qr = a0.Q + rb * QW;
+  double* mdr = a0.md + rb;
+  float* atdr = a0.atd + rb;
+  const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
+
+  // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
+  // Agent slots are branch-free: a slot past the tile's last agent SHADOWS the
+  // tile's first agent (same inputs, so every value it computes and stores is
+  // bit-identical to the owner's); only its history contributions are masked
+  // (vm = 0).  Per-slot branches cost more in exec-mask and copy instructions.
+  // slot u: (r << 16) | (c << 8) | its action bits (a | s_old << 1 | dp << 2 | s_t << 3 | s' << 4, set
+  // from phase 1b on); the agent index is agent_of(rc[u]) (recomputed, not held)
+  // (PERSIST: q, qb, md_own, atd_own and the slots carry over from one iteration to the next)
+  int rc[APT];
+  unsigned vbits = 0;  // bit u: slot u holds an owned agent
+  double q[APT][4];
+  double qb[APT][QB ? 4 : 1];
+  double md_own[APT];
+  float atd_own[APT];
+  const int n_own = th * tw;
+  const uint32_t g00 = (uint32_t)(y0 * L + x0);
+  // (row < 256, L < 2^24: a full-rate 24-bit multiply instead of the quarter-rate 32-bit one)
+  auto agent_of = [&](int rcu) { return g00 + __umul24((uint32_t)(rcu >> 16), (uint32_t)L) + ((rcu >> 8) & 0xff); };
+  bool stored = false;  // PERSIST: the table is in memory (absorbing iteration, or a failed wait)
+  int t = t0;
+  for (;; ++t) {
+  // the iteration's arguments: the halves of the ping-pong buffers and the draw record of t
+  TileArgs a = a0;
+  if constexpr (PERSIST) {
+    const int cur = (t - 1) & 1, nxt = t & 1;
+    a.S_in = pa.S[cur];
+    a.S_out = pa.S[nxt];
+    a.R_in = pa.R[cur];
+    a.R_out = pa.R[nxt];
+    a.pub_in = pa.pub[cur];
+    a.pub_out = pa.pub[nxt];
+    if (pa.draws0) a.draws = pa.draws0 + (size_t)((t - 1) % pa.draw_slots) * pa.draw_stride;
+  }
+  const bool first = !PERSIST || t == t0;  // the launch's first iteration: load the carried state
+  // the thread index, opaque per iteration in a persistent launch: values derived from it (window
+  // and record addresses, slot tables) are recomputed each iteration instead of being hoisted out
+  // of the loop and held -- or spilled -- across it (the carried Q rows need those registers)
+  int tid = threadIdx.x;
+  if constexpr (PERSIST) asm volatile("" : "+v"(tid));
   const uint8_t* Sin = a.S_in + rb;
   uint8_t* Sout = a.S_out + rb;
   const RT* Rin = reinterpret_cast<const RT*>(a.R_in) + rb;
   RT* Rout = reinterpret_cast<RT*>(a.R_out) + rb;
   const bool pending = t > 1;
-  const int tid = threadIdx.x;
-  const int aw = tw + 2 * HA, ah = th + 2 * HA;  // region: tile + ring
   STAMP(0);
 #if SPGG_STAMPS
   if (t == SPGG_STAMP_T && tid == 0 && stamp_id < kStampWG) {
@@ -953,24 +1123,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   // None of these loads depends on the replica's state, so they are all in
   // flight together (one memory round trip) while the scalar reads below
   // (stop flag, counters, parameters) resolve.
-  // Owned agent u of this thread: tile-local k = tid + u*kBlock, (r, c) packed.
-  // Agent slots are branch-free: a slot past the tile's last agent SHADOWS the
-  // tile's first agent (same inputs, so every value it computes and stores is
-  // bit-identical to the owner's); only its history contributions are masked
-  // (vm = 0).  Per-slot branches cost more in exec-mask and copy instructions.
-  // slot u: (r << 16) | (c << 8) | its action bits (a | s_old << 1 | dp << 2 | s_t << 3 | s' << 4, set
-  // from phase 1b on); the agent index is agent_of(rc[u]) (recomputed, not held)
-  int rc[APT];
-  unsigned vbits = 0;  // bit u: slot u holds an owned agent
-  double q[APT][4];
-  double qb[APT][QB ? 4 : 1];
-  double md_own[APT];
-  float atd_own[APT];
-  const int n_own = th * tw;
-  const uint32_t g00 = (uint32_t)(y0 * L + x0);
-  // (row < 256, L < 2^24: a full-rate 24-bit multiply instead of the quarter-rate 32-bit one)
-  auto agent_of = [&](int rcu) { return g00 + __umul24((uint32_t)(rcu >> 16), (uint32_t)L) + ((rcu >> 8) & 0xff); };
-  {
+  if (!first) {
+#pragma unroll
+    for (int u = 0; u < APT; ++u) rc[u] &= ~0xff;  // the last iteration's action bits
+  } else {
     const int dr = kBlock / tw, dc = kBlock - (kBlock / tw) * tw;
     int r = tid / tw, c = tid - (tid / tw) * tw;
 #pragma unroll
@@ -1027,17 +1183,17 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   DwordWindow<JRD, DWR> winRd;
   RowWindow<JRR, TWC + 2 * HA, RT> winR;
   if constexpr (TWC > 0) {
-    winS.load(Sin, th + 2 * HS, y0 - HS, (x0 - HS) & ~3, L);
+    winS.template load<PERSIST>(Sin, th + 2 * HS, y0 - HS, (x0 - HS) & ~3, L, tid);
     if constexpr (!AS) {
-      if constexpr (RQ) winRd.load(Rin, ah, y0 - HA, (x0 - HA) & ~3, L);
-      else winR.load(Rin, ah, y0 - HA, x0 - HA, L);
+      if constexpr (RQ) winRd.template load<PERSIST>(Rin, ah, y0 - HA, (x0 - HA) & ~3, L, tid);
+      else winR.template load<PERSIST>(Rin, ah, y0 - HA, x0 - HA, L, tid);
     }
   }
 
   // the pending NI record after every other load (its address waits for the replica's kappa): a
   // replica with kappa == 0 never uses it (phase 1a skips the NI term), so all its lanes read
   // the replica's first entry -- one cache line per wave instead of 12 B per agent
-  if (!(SPGG_ABLATE & 512) && !RECOMP) {
+  if (!(SPGG_ABLATE & 512) && !RECOMP && first) {
     const bool ni_rec = __builtin_amdgcn_readfirstlane((int)(a.params[rep].kappa != 0.0)) != 0;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
@@ -1061,7 +1217,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     dw1 = *at(a.draws, wi + 1);
   }
   // replica state (scalar loads)
-  const int st = a.stop_iter[rep];
+  const int st = first ? a.stop_iter[rep] : 0;  // (PERSIST: stops within the launch end its loop)
   const bool dead = st != 0 && st < t;  // absorbed before t: nothing to do
   const spgg_rep_params& pg = a.params[rep];
   // the replica's parameters (per-agent fields read from LDS: through a reference into global
@@ -1084,16 +1240,27 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   const double* rrow = a.stats + (size_t)rep * a.stripes * stripe_len;
   double* srow = a.stats + ((size_t)rep * a.stripes + tile % a.stripes) * stripe_len;
   bool stop_now = false;
-  if (!fin_only) {
-    double nc = 0.0;
-    for (int k = 0; k < a.stripes; ++k) nc += rrow[k * stripe_len + (size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
+  double gmax_prev = 0.0;
+  if constexpr (PERSIST) {
+    // written by this launch's previous iteration (other workgroups' atomics): sc1 vector loads,
+    // stripe k in lane k; NCOOP sums integers (exact in any order), the maximum is order-free
+    const int lane = tid & 63, k = lane < a.stripes ? lane : 0;
+    const double ncv = hload<true>(rrow + k * stripe_len + (size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP);
+    const double gmv = pending ? hload<true>(rrow + k * stripe_len + (size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX) : 0.0;
+    const double nc = uniform_f64(wave_sum(lane < a.stripes ? ncv : 0.0));
     stop_now = (nc == 0.0) || (nc == (double)n);  // spgg.py:405
+    gmax_prev = uniform_f64(max_f64(wave_max(gmv), 0.0));
+  } else {
+    if (!fin_only) {
+      double nc = 0.0;
+      for (int k = 0; k < a.stripes; ++k) nc += rrow[k * stripe_len + (size_t)t * SPGG_NSTAT + SPGG_ST_NCOOP];
+      stop_now = (nc == 0.0) || (nc == (double)n);  // spgg.py:405
+    }
+    if (pending)
+      for (int k = 0; k < a.stripes; ++k)
+        gmax_prev = fmax(gmax_prev, rrow[k * stripe_len + (size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX]);
   }
   const bool acting = !fin_only && !stop_now;
-  double gmax_prev = 0.0;
-  if (pending)
-    for (int k = 0; k < a.stripes; ++k)
-      gmax_prev = fmax(gmax_prev, rrow[k * stripe_len + (size_t)(t - 1) * SPGG_NSTAT + SPGG_ST_GMAX]);
   const double lam_den = uniform_f64(pending ? gmax_prev + pg.lambda_eps : 1.0);
   const double lam_rcp = uniform_f64(1.0 / lam_den);  // IEEE, once per workgroup
   const double eps_t = a.eps[(size_t)rep * a.slots + t];
@@ -1107,10 +1274,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   if (tid < kParamWords) reinterpret_cast<uint64_t*>(&hps)[tid] = pword;
   else if (tid < kParamWords + 12) reinterpret_cast<uint64_t*>(tab)[tid - kParamWords] = pword;
   if constexpr (TWC > 0) {
-    winS.store(sS, ly.sw, th + 2 * HS, sD);
+    winS.store(sS, ly.sw, th + 2 * HS, sD, tid);
     if constexpr (!AS) {
-      if constexpr (RQ) winRd.store(reinterpret_cast<uint8_t*>(sR), ly.aw, ah, nullptr);
-      else winR.template store<(TWC + 2 * HS + 6) / 4 * 4>(sR, ah, nullptr);
+      if constexpr (RQ) winRd.store(reinterpret_cast<uint8_t*>(sR), ly.aw, ah, nullptr, tid);
+      else winR.template store<(TWC + 2 * HS + 6) / 4 * 4>(sR, ah, nullptr, tid);
     }
   } else {
     stage_region<JSF>(sS, ly.sw, Sin, th + 2 * HS, tw + 2 * HS, y0 - HS, x0 - HS, L, tiny, sD);
@@ -1133,7 +1300,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
 #pragma unroll
     for (int j = 0; j < RP; ++j)
 #pragma unroll
-      for (int f = 0; f < PF; ++f) rv[j][f] = *at(pin, (uint32_t)(re[j].y + f * a.PB));
+      for (int f = 0; f < PF; ++f) rv[j][f] = hload<PERSIST>(at(pin, (uint32_t)(re[j].y + f * a.PB)));
   }
   __syncthreads();
   STAMP(1);
@@ -1153,15 +1320,15 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
   }
   // plus counts for the payoffs of phases 1b / 1c (their barrier: after phase 1a)
   if (!fin_only) {
-    if constexpr (TWC > 0) build_plus_counts_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPC, sD, ly.sw, ah + 2, soffS);
-    else build_plus_counts(sPC, sDv, ly.sw, ah + 2);
+    if constexpr (TWC > 0) build_plus_counts_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPC, sD, ly.sw, ah + 2, soffS, tid);
+    else build_plus_counts(sPC, sDv, ly.sw, ah + 2, tid);
   }
   // the rewards of iteration t-1 over the region (tile + ring), into sRew (phase 1a reads them;
   // phases 1b / 1c overwrite them with iteration t's after the barrier that ends phase 1a)
   const bool rec_prev = RECOMP && pending && kappa != 0.0;  // workgroup-uniform
   if (rec_prev) {
-    if constexpr (TWC > 0) build_plus_counts_prev_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPP, sS, ly.sw, ah + 2, soffS);
-    else build_plus_counts_prev(sPP, sSv, ly.sw, ah + 2);
+    if constexpr (TWC > 0) build_plus_counts_prev_dw<(TWC + 2 * HA + 2 + 3) / 4>(sPP, sS, ly.sw, ah + 2, soffS, tid);
+    else build_plus_counts_prev(sPP, sSv, ly.sw, ah + 2, tid);
     __syncthreads();  // both plus-count planes
     const int dr = kBlock / aw, dc = kBlock - (kBlock / aw) * aw;
     int ry = tid / aw, rx = tid - (tid / aw) * aw;
@@ -1269,12 +1436,13 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
         }
       }
     }
-    wave_partials<8>(v, red, 0);
+    wave_partials<8>(v, red, 0, tid);
     pct_t1 = pct;  // reduced with phase 1b's values
   }
   if (!acting) {  // flush launch or absorbing iteration: persist the finalized Q
 #pragma unroll
     for (int u = 0; u < APT; ++u) store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u]);
+    stored = true;
   }
   // the ring cells' border records (landed during phase 1a) to LDS for phase 1c:
   // held in registers across phase 1b they cost the occupancy of a fifth wave
@@ -1320,7 +1488,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       const int s_t = (rc[u] >> 3) & 1;                     // (S_t bits, recorded in phase 1a)
       const double P = payoff_pc(sPC, r + HA, c + HA, tab + (s_t ? 6 : 0), hp.norm_min, hp.norm_den,
                                  hp.norm_rcp);
-      const RVal<RQ> r_t = AS ? *at(Rin, agent_of(rc[u])) : sRv[ca];
+      const RVal<RQ> r_t = AS ? hload<PERSIST>(at(Rin, agent_of(rc[u]))) : sRv[ca];
       if constexpr (RQ) rsum += one ? r_t : 0;             // spgg.py:394 (units)
       else rsum = __builtin_fma(r_t, vmu, rsum);
       if (!acting) continue;
@@ -1364,7 +1532,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     va[0] = (double)rsum;
     va[3] = (double)pct_t1;
     // red[wave*64 + 16..19]: va[0..3] (reduced here: frees their registers for phases 1c / 2)
-    if (!(SPGG_ABLATE & (8 | 65536))) wave_partials<4>(va, red, 16);
+    if (!(SPGG_ABLATE & (8 | 65536))) wave_partials<4>(va, red, 16, tid);
   }
   STAMP(3);
 
@@ -1444,9 +1612,10 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       double rn0, rn1;  // row s_{t+1} of the updated table (the border record's)
       const float atd = td_update<ALG, RNG>(a, hp, rep, agent_of(rc[u]), t, pkey, eps_t, eps53, diag_on, rew, so,
                                             act, sn, q[u], qb[u], &rn0, &rn1);
-      if (diag_on && !(SPGG_ABLATE & (256 | 2048))) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
+      if constexpr (PERSIST) atd_own[u] = atd;  // (carried to the next iteration's phase 1a)
+      else if (diag_on && !(SPGG_ABLATE & (256 | 2048))) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
       // the rows this launch changed: the TD row (so) and the NI row of t-1 (phase 1a)
-      if (!(SPGG_ABLATE & 2048)) {
+      if (!PERSIST && !(SPGG_ABLATE & 2048)) {
         uint32_t rows = ((ni_rows >> (2 * u)) & 3u) | (1u << so);
 #if SPGG_QSTORE == 1
         rows = 3u;
@@ -1488,19 +1657,20 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
       bmax = max_f64(bmax, mdp);
       // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
       // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)
-      if (ni_on && !RECOMP && !(SPGG_ABLATE & (2048 | 8192))) *at(mdr, agent_of(rc[u])) = mdp;
-      *at(Sout, agent_of(rc[u])) = (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4));
-      *at(Rout, agent_of(rc[u])) = sRn[ca];
+      if constexpr (PERSIST) md_own[u] = mdp;
+      else if (ni_on && !RECOMP && !(SPGG_ABLATE & (2048 | 8192))) *at(mdr, agent_of(rc[u])) = mdp;
+      hstore<PERSIST>(at(Sout, agent_of(rc[u])), (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4)));
+      hstore<PERSIST>(at(Rout, agent_of(rc[u])), (RT)sRn[ca]);
       const int bslot = (int)(int16_t)(uint16_t)(bsw >> (16 * u));  // (table: border_slot_table)
       if (bslot >= 0) {  // row s_{t+1} + max_diff for the neighbours' ring
         double* rec = pout + bslot;
-        rec[0] = rn0;
-        rec[a.PB] = rn1;
+        hstore<PERSIST>(rec, rn0);
+        hstore<PERSIST>(rec + a.PB, rn1);
         if constexpr (QB) {
-          rec[2 * a.PB] = sn ? qb[u][QB ? 2 : 0] : qb[u][0];
-          rec[3 * a.PB] = sn ? qb[u][QB ? 3 : 0] : qb[u][QB ? 1 : 0];
+          hstore<PERSIST>(rec + 2 * a.PB, sn ? qb[u][QB ? 2 : 0] : qb[u][0]);
+          hstore<PERSIST>(rec + 3 * a.PB, sn ? qb[u][QB ? 3 : 0] : qb[u][QB ? 1 : 0]);
         }
-        if (ni_on) rec[(PF - 1) * a.PB] = mdp;
+        if (ni_on) hstore<PERSIST>(rec + (PF - 1) * a.PB, mdp);
       }
       // group composition on S_{t+1}, spgg.py:585-592: nibble nd of gcn
       const int nd = act + an[0] + an[1] + an[2] + an[3];   // (the four axial neighbours, loaded above)
@@ -1521,7 +1691,7 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
                       (gcn >> 20) & 0xfu,
                       0u,
                       0u};
-    wave_partials<8>(cw, red, 24);
+    wave_partials<8>(cw, red, 24, tid);
   }
   {  // the tile's max(0, max_diff): wave maxima -> red[wave*64 + 12]
     const double wm = wave_max(bmax);
@@ -1611,6 +1781,42 @@ __global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_ste
     }
   }
   STAMP(7);
+  if constexpr (!PERSIST) {
+    break;
+  } else {
+    if (!acting || t == pa.t_end) break;  // absorbed (the table stored in phase 1a), or done
+    if (!replica_barrier(pa, rep, tile, a0.tiles_per_rep, (uint32_t)(t - t0 + 1))) {
+      stored = true;  // a tile never arrived: stop here (SPGG_STEP_ERR_BARRIER; the state is void)
+      break;
+    }
+  }
+  }  // iterations
+  if constexpr (PERSIST) {
+    if (!stored) {  // the carried state after the launch's last iteration, as a launch leaves it
+      const bool ni_rec = __builtin_amdgcn_readfirstlane((int)(a0.params[rep].kappa != 0.0)) != 0;
+#pragma unroll
+      for (int u = 0; u < APT; ++u) {
+        store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u]);
+        if (!RECOMP && ni_rec) {
+          *at(mdr, agent_of(rc[u])) = md_own[u];
+          *at(atdr, agent_of(rc[u])) = atd_own[u];
+        }
+      }
+    }
+  }
+}
+
+template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
+__global__ __launch_bounds__(kBlock, min_waves(M2, RNG, TWC, ALG)) void spgg_step_kernel(TileArgs a, int t,
+                                                                                         int fin_only) {
+  step_impl<M2, AS, RQ, RNG, APT, TWC, ALG, false>(a, t, fin_only, spgg_impl::PersistArgs{});
+}
+
+// The persistent form: four workgroups per CU at most 128 VGPRs (cfg5's 1000 tiles of 1024
+// agents must all be resident on 256 CUs).
+template <bool M2, bool AS, bool RQ, int RNG, int APT, int TWC, int ALG>
+__global__ __launch_bounds__(kBlock, 4) void spgg_persist_kernel(TileArgs a, int t0, spgg_impl::PersistArgs pa) {
+  step_impl<M2, AS, RQ, RNG, APT, TWC, ALG, true>(a, t0, 0, pa);
 }
 
 // Prologue of iteration 1: state s_1 of every agent into S_1 bit 4 and the
@@ -1693,6 +1899,41 @@ __global__ __launch_bounds__(kBlock) void spgg_publish_init_kernel(TileArgs a) {
 
 namespace spgg_impl {
 
+// The persistent instance for lc (compile-time-width tiles: the operator's maximum agents per
+// thread at width 40, or two at width 20), or null.
+template <bool M2, bool AS, bool RQ, int RNG, int ALG>
+const void* persist_fn_t(const LaunchCfg& lc) {
+  constexpr int APT = apt_of(ALG);
+  if constexpr (APT > 2) {
+    if (lc.apt == 2 && lc.twc == 20)
+      return reinterpret_cast<const void*>(&spgg_persist_kernel<M2, AS, RQ, RNG, 2, 20, ALG>);
+  }
+  if (lc.apt == APT && lc.twc == 40)
+    return reinterpret_cast<const void*>(&spgg_persist_kernel<M2, AS, RQ, RNG, APT, 40, ALG>);
+  return nullptr;
+}
+
+template <int ALG>
+const void* persist_fn(const LaunchCfg& lc) {
+  if (lc.rng == SPGG_RNG_INJECT) return nullptr;  // (one iteration per call)
+  const bool ph = lc.rng == SPGG_RNG_PHILOX;
+#define SPGG_PF(X, Y, Z)                                                                             \
+  if (lc.m2 == X && lc.as == Y && lc.rq == Z)                                                        \
+    return ph ? persist_fn_t<X, Y, Z, SPGG_RNG_PHILOX, ALG>(lc) : persist_fn_t<X, Y, Z, SPGG_RNG_MT19937, ALG>(lc);
+  SPGG_PF(0, 0, 0) SPGG_PF(0, 0, 1) SPGG_PF(0, 1, 0) SPGG_PF(0, 1, 1)
+  SPGG_PF(1, 0, 0) SPGG_PF(1, 0, 1) SPGG_PF(1, 1, 0) SPGG_PF(1, 1, 1)
+#undef SPGG_PF
+  return nullptr;
+}
+
+template <int ALG>
+int persist_blocks_per_cu(const LaunchCfg& lc) {
+  const void* f = persist_fn<ALG>(lc);
+  int nb = 0;
+  if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlock, lc.lds_bytes) != hipSuccess) return 0;
+  return nb;
+}
+
 template <bool M2, bool AS, bool RQ, int RNG, int ALG>
 void launch_t(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
   constexpr int APT = apt_of(ALG);
@@ -1741,7 +1982,17 @@ void launch_rq(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream
 }
 
 template <int ALG>
-void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s) {
+void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStream_t s, const PersistArgs* pa) {
+  if (pa) {  // iterations t .. pa->t_end in one launch (the host checked the instance and residency)
+    const void* f = persist_fn<ALG>(lc);
+    if (!f) return;  // (spgg_step only asks for instances persist_blocks_per_cu found)
+    TileArgs ka = a;
+    int kt = t;
+    PersistArgs kp = *pa;
+    void* args[] = {&ka, &kt, &kp};
+    (void)hipLaunchKernel(f, dim3(((lc.total_tiles + 7) / 8) * 8), dim3(kBlock), args, lc.lds_bytes, s);
+    return;
+  }
   if (lc.m2) {
     if (lc.as) launch_rq<true, true, ALG>(lc, a, t, fin, s);
     else launch_rq<true, false, ALG>(lc, a, t, fin, s);
@@ -1754,9 +2005,12 @@ void launch_alg(const LaunchCfg& lc, const TileArgs& a, int t, int fin, hipStrea
 // Explicit instantiation in the operator's own translation unit; elsewhere
 // an extern declaration keeps the kernels from being instantiated again.
 #define SPGG_LAUNCH_INST(k, name)                                                                   \
-  template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t);
+  template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t, const PersistArgs*); \
+  template int persist_blocks_per_cu<name>(const LaunchCfg&);
 #define SPGG_LAUNCH_EXTERN(k, name)                                                                 \
-  extern template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t);
+  extern template void launch_alg<name>(const LaunchCfg&, const TileArgs&, int, int, hipStream_t,   \
+                                        const PersistArgs*);                                        \
+  extern template int persist_blocks_per_cu<name>(const LaunchCfg&);
 #if SPGG_TU_HAS_ALG(0)
 #if SPGG_STAMPS
 }  // namespace spgg_impl
@@ -2305,6 +2559,12 @@ struct spgg_ctx {
   int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4, PB = 0;
   int stripes = 1;  // history-record stripes per replica
   size_t lds_bytes = 0;
+  // persistent launches (spgg_persist_kernel): decided at spgg_create from the whole batch's
+  // tiles and the instance's occupancy; arrival counters [n_rep][stripes][kBarWords]
+  bool persist = false;
+  int persist_capacity = 0;      // workgroups the device holds at once (occupancy x CUs)
+  uint32_t* d_bar = nullptr;
+  uint32_t bar_base = 0;         // barrier rounds of this run's earlier persistent launches
   std::string err;
 };
 
@@ -2553,8 +2813,7 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   return a;
 }
 
-void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
-  const TileArgs a = make_args(c, t);
+spgg_impl::LaunchCfg launch_cfg(const spgg_ctx* c) {
   spgg_impl::LaunchCfg lc;
   lc.m2 = c->cfg.second_order != 0;
   lc.as = c->cfg.state_mode == SPGG_STATE_ACTION;
@@ -2564,12 +2823,83 @@ void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s) {
   lc.apt = c->apt;
   lc.total_tiles = c->cfg.n_rep * c->tiles_per_rep;
   lc.lds_bytes = c->lds_bytes;
+  return lc;
+}
+
+void launch_step(const spgg_ctx* c, int t, int fin, hipStream_t s, const spgg_impl::PersistArgs* pa = nullptr) {
+  const TileArgs a = make_args(c, t);
+  const spgg_impl::LaunchCfg lc = launch_cfg(c);
   switch (c->cfg.algorithm) {
-    case SPGG_ALG_SARSA: spgg_impl::launch_alg<SPGG_ALG_SARSA>(lc, a, t, fin, s); break;
-    case SPGG_ALG_EXPECTED_SARSA: spgg_impl::launch_alg<SPGG_ALG_EXPECTED_SARSA>(lc, a, t, fin, s); break;
-    case SPGG_ALG_DOUBLE_Q: spgg_impl::launch_alg<SPGG_ALG_DOUBLE_Q>(lc, a, t, fin, s); break;
-    default: spgg_impl::launch_alg<SPGG_ALG_QLEARNING>(lc, a, t, fin, s); break;
+    case SPGG_ALG_SARSA: spgg_impl::launch_alg<SPGG_ALG_SARSA>(lc, a, t, fin, s, pa); break;
+    case SPGG_ALG_EXPECTED_SARSA: spgg_impl::launch_alg<SPGG_ALG_EXPECTED_SARSA>(lc, a, t, fin, s, pa); break;
+    case SPGG_ALG_DOUBLE_Q: spgg_impl::launch_alg<SPGG_ALG_DOUBLE_Q>(lc, a, t, fin, s, pa); break;
+    default: spgg_impl::launch_alg<SPGG_ALG_QLEARNING>(lc, a, t, fin, s, pa); break;
   }
+}
+
+// Workgroups of the context's persistent instance one CU holds (0: none for this layout).
+int persist_blocks(const spgg_ctx* c) {
+  const spgg_impl::LaunchCfg lc = launch_cfg(c);
+  switch (c->cfg.algorithm) {
+    case SPGG_ALG_SARSA: return spgg_impl::persist_blocks_per_cu<SPGG_ALG_SARSA>(lc);
+    case SPGG_ALG_EXPECTED_SARSA: return spgg_impl::persist_blocks_per_cu<SPGG_ALG_EXPECTED_SARSA>(lc);
+    case SPGG_ALG_DOUBLE_Q: return spgg_impl::persist_blocks_per_cu<SPGG_ALG_DOUBLE_Q>(lc);
+    default: return spgg_impl::persist_blocks_per_cu<SPGG_ALG_QLEARNING>(lc);
+  }
+}
+
+// Error word (and its pinned host copy) of a context, for the generator and persistent launches.
+int err_word_init(spgg_ctx* c) {
+  int rc = SPGG_OK;
+  if (!c->d_err) {
+    rc = hip_check(c, hipMalloc(&c->d_err, 4), "hipMalloc(err)");
+    if (!rc) rc = hip_check(c, hipMemset(c->d_err, 0, 4), "hipMemset(err)");
+  }
+  if (!rc && !c->h_err) {
+    void* h = nullptr;
+    rc = hip_check(c, hipHostMalloc(&h, 4, hipHostMallocDefault), "hipHostMalloc(err)");
+    if (!rc) {
+      c->h_err = static_cast<volatile uint32_t*>(h);
+      *c->h_err = 0;
+    }
+  }
+  return rc;
+}
+
+// The persistent launch's arrival counters and error word (once per context).
+int persist_lazy_init(spgg_ctx* c) {
+  int rc = err_word_init(c);
+  if (rc || c->d_bar) return rc;
+  const size_t bytes = (size_t)c->cfg.n_rep * c->stripes * spgg_impl::kBarWords * 4;
+  rc = hip_check(c, hipMalloc(&c->d_bar, bytes), "hipMalloc(barrier counters)");
+  if (!rc) rc = hip_check(c, hipMemset(c->d_bar, 0, bytes), "hipMemset(barrier counters)");
+  return rc;
+}
+
+// Iterations t .. t1 (t1 > t) as ONE persistent launch; a run's first one zeroes the counters.
+void launch_persist(spgg_ctx* c, int t, int t1, hipStream_t s) {
+  if (t == 1) {
+    (void)hipMemsetAsync(c->d_bar, 0, (size_t)c->cfg.n_rep * c->stripes * spgg_impl::kBarWords * 4, s);
+    c->bar_base = 0;
+  }
+  spgg_impl::PersistArgs pa{};
+  for (int i = 0; i < 2; ++i) {
+    pa.S[i] = c->buf.S[i];
+    pa.R[i] = c->buf.R[i];
+    pa.pub[i] = c->buf.pub[i];
+  }
+  pa.draws0 = c->cfg.rng_mode == SPGG_RNG_PHILOX ? nullptr : c->buf.draws;
+  pa.draw_stride = c->buf.draw_slot_stride;
+  pa.draw_slots = c->draw_slots;
+  pa.t_end = t1;
+  pa.bar = c->d_bar;
+  pa.shards = c->stripes;
+  pa.base = c->bar_base;
+  pa.err = c->d_err;
+  launch_step(c, t, 0, s, &pa);
+  c->bar_base += (uint32_t)(t1 - t);
+  // the error word after the launch, for spgg_status (no host sync)
+  (void)hipMemcpyAsync((void*)c->h_err, c->d_err, 4, hipMemcpyDeviceToHost, s);
 }
 
 // q: the chunk a pipelined launch generates (-1: a single-chain launch in place on mt_state)
@@ -2655,16 +2985,7 @@ int mt_lazy_init(spgg_ctx* c) {
   }
   if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->gen_idle, hipEventDisableTiming), "hipEventCreate");
   if (!rc) rc = hip_check(c, hipEventCreateWithFlags(&c->caller_ready, hipEventDisableTiming), "hipEventCreate");
-  if (!rc) rc = hip_check(c, hipMalloc(&c->d_err, 4), "hipMalloc(gen err)");
-  if (!rc) rc = hip_check(c, hipMemset(c->d_err, 0, 4), "hipMemset(gen err)");
-  if (!rc) {
-    void* h = nullptr;
-    rc = hip_check(c, hipHostMalloc(&h, 4, hipHostMallocDefault), "hipHostMalloc(gen err)");
-    if (!rc) {
-      c->h_err = static_cast<volatile uint32_t*>(h);
-      *c->h_err = 0;
-    }
-  }
+  if (!rc) rc = err_word_init(c);
   if (rc || c->chains == 1) return rc;
   // chained generator: start windows, chunk keys, and the jump polynomials
   const size_t R = c->cfg.n_rep, win = R * c->chains * spgg_mt::kSplits * 624;
@@ -2834,6 +3155,19 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
                              (size_t)(ly.ah + 2) * kPcPitch);
     if (c->lds_bytes > 160 * 1024) rc = fail(c, SPGG_E_ARG, "tile LDS footprint exceeds 160 KB");
   }
+  // persistent launches: when the whole batch's tiles (every replica group of it, which run
+  // concurrently) fit the device at once -- the persistent instance's occupancy x CUs -- each
+  // spgg_step call (each generator chunk, MT19937) is one launch instead of one per iteration
+  if (!rc && cfg->rng_mode != SPGG_RNG_INJECT) {
+    const char* e = tuning_env("SPGG_PERSIST");  // "0": one launch per iteration
+    const int nb = (e && !strcmp(e, "0")) ? 0 : persist_blocks(c);
+    int cus = 0;
+    if (nb > 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess) {
+      const long long reps = cfg->batch_reps > 0 ? cfg->batch_reps : cfg->n_rep;
+      c->persist_capacity = nb * cus;
+      c->persist = reps * c->tiles_per_rep <= (long long)c->persist_capacity;
+    }
+  }
   if (rc) {
     g_create_err = c->err;
     spgg_destroy(c);
@@ -2902,14 +3236,20 @@ static int step_check(spgg_ctx* c, int32_t t0, int32_t n_steps) {
 }
 
 // Run setup of a checked spgg_step call: the iteration-1 prologue and the generator's start.
+// The fallible setup a step needs (allocations, the generator's jump polynomials), idempotent.
+static int step_setup(spgg_ctx* c) {
+  int rc = SPGG_OK;
+  if (c->cfg.rng_mode == SPGG_RNG_MT19937) rc = mt_lazy_init(c);
+  if (!rc && c->persist) rc = persist_lazy_init(c);
+  return rc;
+}
+
 static int step_begin(spgg_ctx* c, int32_t t0, int32_t n_steps, hipStream_t s) {
   if (t0 == 1) c->params_moved = false;  // a new run
   const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
-  if (mt) {
-    int rc = mt_lazy_init(c);
-    if (rc) return rc;
-    if (t0 == 1) c->gen_upto = 0;  // a new run: generation restarts from mt_state
-  }
+  int rc = step_setup(c);
+  if (rc) return rc;
+  if (mt && t0 == 1) c->gen_upto = 0;  // a new run: generation restarts from mt_state
   if (t0 == 1 && n_steps > 0) launch_step(c, 0, 0, s);  // iteration-1 prologue
   if (mt && n_steps > 0 && c->gen_upto == 0) {
     // a run's first generator chunks read mt_state, eps and stop_iter and write the draw and
@@ -2921,9 +3261,20 @@ static int step_begin(spgg_ctx* c, int32_t t0, int32_t n_steps, hipStream_t s) {
   return SPGG_OK;
 }
 
-// Iteration t of a spgg_step call that began at t0: its generator chunks (MT19937) and the
-// step launch.
-static void step_iter(spgg_ctx* c, int t, int32_t t0, hipStream_t s) {
+// The last iteration of the segment of a spgg_step call that starts at t (the call ends before
+// end): a persistent context runs to the call's end -- MT19937: to the end of the generator chunk
+// holding t, whose generation the segment's launch waits for -- in one launch; otherwise the
+// segment is iteration t alone.
+static int seg_end(const spgg_ctx* c, int t, int end) {
+  if (!c->persist) return t;
+  int t1 = end - 1;
+  if (c->cfg.rng_mode == SPGG_RNG_MT19937) t1 = std::min(t1, ((t - 1) / c->gen_chunk + 1) * c->gen_chunk);
+  return t1;
+}
+
+// Iterations t .. t1 of a spgg_step call that began at t0: their generator chunks (MT19937) and
+// the step launch(es) -- one per iteration, or one persistent launch.
+static void step_seg(spgg_ctx* c, int t, int t1, int32_t t0, hipStream_t s) {
   const bool mt = c->cfg.rng_mode == SPGG_RNG_MT19937;
   const int K = c->gen_chunk, T = c->cfg.iterations;
   // timing-only builds (-DSPGG_TIMING=1: the step launches skipped, the generator alone; =2: the
@@ -2935,8 +3286,11 @@ static void step_iter(spgg_ctx* c, int t, int32_t t0, hipStream_t s) {
     while (timing != 2 && c->gen_upto < std::min(T, (q + 2) * K)) enqueue_gen_chunk(c, c->gen_upto / K);
     if (timing != 2 && (t == q * K + 1 || t == t0)) (void)hipStreamWaitEvent(s, c->gen_done[q & 1], 0);
   }
-  if (timing != 1) launch_step(c, t, 0, s);
-  if (mt && (t % K == 0 || t == T)) (void)hipEventRecord(c->step_done[((t - 1) / K) & 1], s);
+  if (timing != 1) {
+    if (t1 > t) launch_persist(c, t, t1, s);
+    else launch_step(c, t, 0, s);
+  }
+  if (mt && (t1 % K == 0 || t1 == T)) (void)hipEventRecord(c->step_done[((t1 - 1) / K) & 1], s);
 }
 
 int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
@@ -2944,7 +3298,12 @@ int spgg_step(spgg_ctx* c, int32_t t0, int32_t n_steps, void* stream) {
   if (rc) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if ((rc = step_begin(c, t0, n_steps, s))) return rc;
-  for (int t = t0; t < t0 + n_steps; ++t) step_iter(c, t, t0, s);
+  const int end = t0 + n_steps;
+  for (int t = t0; t < end;) {
+    const int t1 = seg_end(c, t, end);
+    step_seg(c, t, t1, t0, s);
+    t = t1 + 1;
+  }
   return hip_check(c, hipGetLastError(), "spgg_step launch");
 }
 
@@ -2960,7 +3319,7 @@ int spgg_step_groups(spgg_ctx* const* ctxs, void* const* streams, int32_t n_ctx,
     // the fallible part of step_begin (the generator's lazy setup: allocations, the jump
     // polynomials) runs here too, so that nothing is enqueued on any context unless every one
     // of them can start; a failure is reported on that context and on ctxs[0], which callers read
-    if (!rc && ctxs[i]->cfg.rng_mode == SPGG_RNG_MT19937) rc = mt_lazy_init(ctxs[i]);
+    if (!rc) rc = step_setup(ctxs[i]);
     if (rc) {
       if (i > 0) fail(ctxs[0], rc, "spgg_step_groups: context " + std::to_string(i) + ": " + ctxs[i]->err);
       return rc;
@@ -2968,10 +3327,21 @@ int spgg_step_groups(spgg_ctx* const* ctxs, void* const* streams, int32_t n_ctx,
   }
   for (int i = 0; i < n_ctx; ++i) {
     int rc = step_begin(ctxs[i], t0, n_steps, reinterpret_cast<hipStream_t>(streams[i]));
-    if (rc) return rc;  // (cannot fail: mt_lazy_init above already succeeded)
+    if (rc) return rc;  // (cannot fail: step_setup above already succeeded)
   }
-  for (int t = t0; t < t0 + n_steps; ++t)
-    for (int i = 0; i < n_ctx; ++i) step_iter(ctxs[i], t, t0, reinterpret_cast<hipStream_t>(streams[i]));
+  // segments of context 0 (every context of one batch has the same layout, generator chunk and
+  // persistent decision -- all decided from the whole batch); one iteration at a time otherwise
+  bool same = true;
+  for (int i = 1; i < n_ctx; ++i)
+    same &= ctxs[i]->persist == ctxs[0]->persist && ctxs[i]->gen_chunk == ctxs[0]->gen_chunk &&
+            ctxs[i]->cfg.rng_mode == ctxs[0]->cfg.rng_mode;
+  const int end = t0 + n_steps;
+  for (int t = t0; t < end;) {
+    int t1 = same ? seg_end(ctxs[0], t, end) : t;
+    for (int i = 0; i < n_ctx; ++i)
+      step_seg(ctxs[i], t, ctxs[i]->persist ? t1 : t, t0, reinterpret_cast<hipStream_t>(streams[i]));
+    t = t1 + 1;
+  }
   const int rc = hip_check(ctxs[0], hipGetLastError(), "spgg_step_groups launch");
   for (int i = 1; i < n_ctx && rc; ++i) ctxs[i]->err = ctxs[0]->err;
   return rc;
@@ -3070,6 +3440,13 @@ int spgg_stat_stripes(const spgg_ctx* c, int32_t* stripes) {
   return SPGG_OK;
 }
 
+int spgg_persistent(const spgg_ctx* c, int32_t* on, int32_t* capacity) {
+  if (!c || !on || !capacity) return SPGG_E_ARG;
+  *on = c->persist ? 1 : 0;
+  *capacity = c->persist_capacity;
+  return SPGG_OK;
+}
+
 int spgg_tile_shape(const spgg_ctx* c, int32_t* tw, int32_t* th) {
   if (!c || !tw || !th) return SPGG_E_ARG;
   *tw = c->TW;
@@ -3119,7 +3496,7 @@ int spgg_set_draw_stream(spgg_ctx* c, void* stream) {
 
 int spgg_destroy(spgg_ctx* c) {
   if (!c) return SPGG_OK;
-  if (c->d_params || c->d_ring || c->gen_stream || c->gen_done[0] || c->d_err) {
+  if (c->d_params || c->d_ring || c->gen_stream || c->gen_done[0] || c->d_err || c->d_bar) {
     (void)hipSetDevice(c->cfg.device);
     if (c->gen_stream) (void)hipStreamSynchronize(c->gen_stream);  // no generator writes after return
     if (c->d_params) (void)hipFree(c->d_params);
@@ -3137,6 +3514,7 @@ int spgg_destroy(spgg_ctx* c) {
       if (c->d_keybuf[i]) (void)hipFree(c->d_keybuf[i]);
     }
     if (c->d_run_pos0) (void)hipFree(c->d_run_pos0);
+    if (c->d_bar) (void)hipFree(c->d_bar);
     if (c->d_polys) (void)hipFree(c->d_polys);
     if (c->own_gen_stream) (void)hipStreamDestroy(c->gen_stream);
   }

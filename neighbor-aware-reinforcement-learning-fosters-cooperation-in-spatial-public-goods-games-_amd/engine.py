@@ -454,6 +454,11 @@ class BatchEngine:
         self.ctx = self.groups[0]["ctx"]
         self.tile = self.layout[0]
         self.mt_layout = self.layout[4]
+        # persistent launches (spgg_persistent): every tile of the batch fits the device at once, so
+        # each step call (MT19937: each generator chunk of it) is one launch per group
+        on, cap = ctypes.c_int32(), ctypes.c_int32()
+        C.check(self.lib.spgg_persistent(self.ctx, ctypes.byref(on), ctypes.byref(cap)), self.ctx, "spgg_persistent")
+        self.persistent, self.persist_capacity = bool(on.value), int(cap.value)
 
     def _draw_layout(self, ctx):
         """(ring slots, u32 words per replica and slot, key-snapshot slots) of the draw records."""

@@ -17,8 +17,13 @@ _PARAM_KEYS = ("r", "c", "cost", "L", "iterations", "alpha", "gamma", "epsilon",
                "reward_weight_payoff", "rep_gain_C", "state_representation", "algorithm")
 
 
+# fixtures that are not whole reference runs (single operator calls: test_operator_host_cpu.py)
+NOT_RUNS = {"operator_calls"}
+
+
 def case_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    return sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+                  if n not in NOT_RUNS)
 
 
 class Case:

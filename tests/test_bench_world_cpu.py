@@ -46,6 +46,7 @@ def _worker(rank, world, port, q):
         def __init__(self, L, iterations, replicas, replica_offset=0, **kw):
             self.L, self.T, self.R = L, iterations, len(replicas)
             self.resident = self.G = self.waves = 1
+            self.persistent = False
             self.mt_layout = (1, 1)
             self.stop_iter = torch.zeros(self.R, dtype=torch.int32)
             self.st = torch.zeros((self.R, iterations + 2, C.NSTAT), dtype=torch.float64)
@@ -63,6 +64,9 @@ def _worker(rank, world, port, q):
 
         def stats_folded(self):
             return self.st
+
+        def check_status(self):
+            pass
 
         def close(self):
             pass

@@ -130,6 +130,8 @@ struct PersistArgs {
   int shards;
   uint32_t base;
   uint32_t* err;           // error word: SPGG_STEP_ERR_BARRIER when a wait ran out of its bound
+  uint32_t* err_host;      // its pinned host copy (device-mapped), set by the failing workgroup itself:
+                           // spgg_status reads it without a copy enqueued after every launch
 };
 constexpr int kBarWords = 16;
 
@@ -265,14 +267,20 @@ __device__ __forceinline__ T* at(T* base, uint32_t i) {
 // A load / store of element p, plain or (SC1: inside a persistent launch, for bytes another
 // workgroup reads) write-through / past the CU's L1 -- relaxed agent-scope atomics, lowered to
 // global_load / global_store ... sc1 (the hand-off rules: replica_barrier below).
+#ifndef SPGG_PERSIST_PLAIN  // timing variant: plain hand-off accesses (results may be stale: WRONG)
+#define SPGG_PERSIST_PLAIN 0
+#endif
+#ifndef SPGG_PERSIST_NORECOMP  // timing variant: see step_impl's CARRY
+#define SPGG_PERSIST_NORECOMP 0
+#endif
 template <bool SC1, typename T>
 __device__ __forceinline__ T hload(const T* p) {
-  if constexpr (SC1) return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (SC1 && !SPGG_PERSIST_PLAIN) return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else return *p;
 }
 template <bool SC1, typename T>
 __device__ __forceinline__ void hstore(T* p, T v) {
-  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (SC1 && !SPGG_PERSIST_PLAIN) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
 
@@ -896,6 +904,9 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+#ifndef SPGG_BAR_DEBUG
+#define SPGG_BAR_DEBUG 0
+#endif
 // Bound of a persistent launch's wait for its replica's other tiles, in polls (each an sc1
 // load round trip, >= ~0.5 us, plus s_sleep): >= ~1 s.  Every tile of a persistent launch is
 // co-resident (the host checks the batch against the instance's occupancy), so a wait that
@@ -907,10 +918,12 @@ constexpr uint32_t kBarrierPolls = 1u << 21;
 // has finished its k-th iteration of the launch (its S / R / border-record stores and history
 // atomics drained).  Returns false when this wait, or another workgroup's, ran out of its bound.
 __device__ __forceinline__ bool replica_barrier(const spgg_impl::PersistArgs& pa, int rep, int tile,
-                                                int tiles_per_rep, uint32_t k) {
+                                                int tiles_per_rep, uint32_t k,
+                                                unsigned long long* arrive_stamp = nullptr) {
   __shared__ int bar_ok;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores and atomics have landed
   __syncthreads();                                  // ... and every other wave's
+  if (arrive_stamp && threadIdx.x == 0) *arrive_stamp = __builtin_amdgcn_s_memrealtime();  // (SPGG_STAMPS)
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x, S = pa.shards;
     uint32_t* ctr = pa.bar + (size_t)rep * S * spgg_impl::kBarWords;
@@ -932,7 +945,18 @@ __device__ __forceinline__ bool replica_barrier(const spgg_impl::PersistArgs& pa
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok && lane == 0) atomicOr(pa.err, (uint32_t)SPGG_STEP_ERR_BARRIER);
+    if (!ok && lane == 0) {
+      atomicOr(pa.err, (uint32_t)SPGG_STEP_ERR_BARRIER);
+      __hip_atomic_fetch_or(pa.err_host, (uint32_t)SPGG_STEP_ERR_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#if SPGG_BAR_DEBUG  // diagnostic build: which shard fell short
+    if (!ok) {
+      const uint32_t have = __hip_atomic_load(ctr + j * spgg_impl::kBarWords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int32_t)(have - want) < 0)
+        printf("spgg barrier: rep %d tile %d k %u shard %d have %u want %u base %u\n", rep, tile, k, j, have, want,
+               pa.base);
+    }
+#endif
     if (lane == 0) bar_ok = ok ? 1 : 0;
   }
   __syncthreads();
@@ -962,12 +986,14 @@ __device__ __forceinline__ bool replica_barrier(const spgg_impl::PersistArgs& pa
 #ifndef SPGG_STAMP_T
 #define SPGG_STAMP_T 30
 #endif
-constexpr int kStampWG = 8192;
-__device__ unsigned long long spgg_stamps[kStampWG * 10];
+// slots per workgroup: 0-7 phases, 8 HW_ID, 9 XCC_ID; persistent launches: 10 = the replica
+// barrier's stores drained (arrival), 11 = its wait passed
+constexpr int kStampWG = 8192, kStampSlots = 12;
+__device__ unsigned long long spgg_stamps[kStampWG * kStampSlots];
 #define STAMP(k)                                                                            \
   do {                                                                                      \
     if (t == SPGG_STAMP_T && tid == 0 && stamp_id < kStampWG)                               \
-      spgg_stamps[stamp_id * 10 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+      spgg_stamps[stamp_id * kStampSlots + (k)] = __builtin_amdgcn_s_memrealtime();         \
   } while (0)
 #else
 #define STAMP(k) \
@@ -1011,7 +1037,10 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
   // it saves bound the launch (cfg3 65.5 -> 64.1 us/step in the driver's window, 54.2 -> 53.2
   // steady); the latency-bound small batches (two / one agent per thread) keep the stored record,
   // where the region pass's VALU sits on the critical path (cfg4 steady 12.2 -> 14.9 us/step)
-  constexpr bool RECOMP = ALG != ALG_SARSA && APT == spgg_impl::apt_of(ALG);
+  constexpr bool RECOMP = ALG != ALG_SARSA && APT == spgg_impl::apt_of(ALG) && !(PERSIST && SPGG_PERSIST_NORECOMP);
+  // PERSIST: the stored pending record (md, atd) of the owned agents carried in registers from one
+  // iteration to the next (timing variant SPGG_PERSIST_NORECOMP: through global memory instead)
+  constexpr bool CARRY = PERSIST && !SPGG_PERSIST_NORECOMP;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   // XCD-aware placement: blocks b, b+8, b+16... share an XCD (round-robin
@@ -1114,8 +1143,8 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    spgg_stamps[stamp_id * 10 + 8] = hw;
-    spgg_stamps[stamp_id * 10 + 9] = xcc;
+    spgg_stamps[stamp_id * kStampSlots + 8] = hw;
+    spgg_stamps[stamp_id * kStampSlots + 9] = xcc;
   }
 #endif
 
@@ -1193,7 +1222,7 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
   // the pending NI record after every other load (its address waits for the replica's kappa): a
   // replica with kappa == 0 never uses it (phase 1a skips the NI term), so all its lanes read
   // the replica's first entry -- one cache line per wave instead of 12 B per agent
-  if (!(SPGG_ABLATE & 512) && !RECOMP && first) {
+  if (!(SPGG_ABLATE & 512) && !RECOMP && (first || !CARRY)) {
     const bool ni_rec = __builtin_amdgcn_readfirstlane((int)(a.params[rep].kappa != 0.0)) != 0;
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
@@ -1612,7 +1641,7 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
       double rn0, rn1;  // row s_{t+1} of the updated table (the border record's)
       const float atd = td_update<ALG, RNG>(a, hp, rep, agent_of(rc[u]), t, pkey, eps_t, eps53, diag_on, rew, so,
                                             act, sn, q[u], qb[u], &rn0, &rn1);
-      if constexpr (PERSIST) atd_own[u] = atd;  // (carried to the next iteration's phase 1a)
+      if constexpr (CARRY) atd_own[u] = atd;  // (carried to the next iteration's phase 1a)
       else if (diag_on && !(SPGG_ABLATE & (256 | 2048))) *at(atdr, agent_of(rc[u])) = atd;  // read only for the NI percent (0 when kappa == 0)
       // the rows this launch changed: the TD row (so) and the NI row of t-1 (phase 1a)
       if (!PERSIST && !(SPGG_ABLATE & 2048)) {
@@ -1657,7 +1686,7 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
       bmax = max_f64(bmax, mdp);
       // max(0, max_diff) feeds only the next launch's NI term, which is +0 when kappa == 0
       // (phase 1a and the ring skip it): not stored then (-8 B/agent-step for those replicas)
-      if constexpr (PERSIST) md_own[u] = mdp;
+      if constexpr (CARRY) md_own[u] = mdp;
       else if (ni_on && !RECOMP && !(SPGG_ABLATE & (2048 | 8192))) *at(mdr, agent_of(rc[u])) = mdp;
       hstore<PERSIST>(at(Sout, agent_of(rc[u])), (uint8_t)((rc[u] & 0xff) | (dp << 2) | (sn << 4)));
       hstore<PERSIST>(at(Rout, agent_of(rc[u])), (RT)sRn[ca]);
@@ -1785,10 +1814,15 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
     break;
   } else {
     if (!acting || t == pa.t_end) break;  // absorbed (the table stored in phase 1a), or done
-    if (!replica_barrier(pa, rep, tile, a0.tiles_per_rep, (uint32_t)(t - t0 + 1))) {
+    unsigned long long* arrive = nullptr;
+#if SPGG_STAMPS
+    if (t == SPGG_STAMP_T && stamp_id < kStampWG) arrive = &spgg_stamps[stamp_id * kStampSlots + 10];
+#endif
+    if (!replica_barrier(pa, rep, tile, a0.tiles_per_rep, (uint32_t)(t - t0 + 1), arrive)) {
       stored = true;  // a tile never arrived: stop here (SPGG_STEP_ERR_BARRIER; the state is void)
       break;
     }
+    STAMP(11);
   }
   }  // iterations
   if constexpr (PERSIST) {
@@ -1797,7 +1831,7 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
 #pragma unroll
       for (int u = 0; u < APT; ++u) {
         store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u]);
-        if (!RECOMP && ni_rec) {
+        if (CARRY && !RECOMP && ni_rec) {
           *at(mdr, agent_of(rc[u])) = md_own[u];
           *at(atdr, agent_of(rc[u])) = atd_own[u];
         }
@@ -2857,7 +2891,8 @@ int err_word_init(spgg_ctx* c) {
   }
   if (!rc && !c->h_err) {
     void* h = nullptr;
-    rc = hip_check(c, hipHostMalloc(&h, 4, hipHostMallocDefault), "hipHostMalloc(err)");
+    // (mapped: a persistent launch's failing workgroup sets it directly, no copy per launch)
+    rc = hip_check(c, hipHostMalloc(&h, 4, hipHostMallocMapped), "hipHostMalloc(err)");
     if (!rc) {
       c->h_err = static_cast<volatile uint32_t*>(h);
       *c->h_err = 0;
@@ -2896,10 +2931,13 @@ void launch_persist(spgg_ctx* c, int t, int t1, hipStream_t s) {
   pa.shards = c->stripes;
   pa.base = c->bar_base;
   pa.err = c->d_err;
+  void* hd = nullptr;
+  pa.err_host = hipHostGetDevicePointer(&hd, (void*)c->h_err, 0) == hipSuccess ? static_cast<uint32_t*>(hd)
+                                                                                 : const_cast<uint32_t*>(c->h_err);
   launch_step(c, t, 0, s, &pa);
   c->bar_base += (uint32_t)(t1 - t);
-  // the error word after the launch, for spgg_status (no host sync)
-  (void)hipMemcpyAsync((void*)c->h_err, c->d_err, 4, hipMemcpyDeviceToHost, s);
+  // (no copy of the error word after the launch: a D2H copy in the stream cost a 20-iteration window
+  // ~150 us; the failing workgroup writes the pinned host word itself, which spgg_status reads)
 }
 
 // q: the chunk a pipelined launch generates (-1: a single-chain launch in place on mt_state)
@@ -3155,16 +3193,20 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
                              (size_t)(ly.ah + 2) * kPcPitch);
     if (c->lds_bytes > 160 * 1024) rc = fail(c, SPGG_E_ARG, "tile LDS footprint exceeds 160 KB");
   }
-  // persistent launches: when the whole batch's tiles (every replica group of it, which run
-  // concurrently) fit the device at once -- the persistent instance's occupancy x CUs -- each
-  // spgg_step call (each generator chunk, MT19937) is one launch instead of one per iteration
+  // persistent launches (opt-in, SPGG_PERSIST=1): when the whole batch's tiles (every replica
+  // group of it, which run concurrently) fit the device at once -- the persistent instance's
+  // occupancy x CUs; MT19937: one workgroup per CU fewer, the room a generator workgroup of the
+  // next chunk takes beside them (with every slot counted, a cfg5 launch waited > 1 s for three
+  // tiles that the generator's workgroups kept from being dispatched) -- each spgg_step call (each
+  // generator chunk, MT19937) is one launch instead of one per iteration.  Off by default: measured
+  // slower on every BASELINE shape ("Persistent launches")
   if (!rc && cfg->rng_mode != SPGG_RNG_INJECT) {
-    const char* e = tuning_env("SPGG_PERSIST");  // "0": one launch per iteration
-    const int nb = (e && !strcmp(e, "0")) ? 0 : persist_blocks(c);
+    const char* e = tuning_env("SPGG_PERSIST");
+    const int nb = (e && !strcmp(e, "1")) ? persist_blocks(c) : 0;
     int cus = 0;
     if (nb > 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess) {
       const long long reps = cfg->batch_reps > 0 ? cfg->batch_reps : cfg->n_rep;
-      c->persist_capacity = nb * cus;
+      c->persist_capacity = (nb - (cfg->rng_mode == SPGG_RNG_MT19937 ? 1 : 0)) * cus;
       c->persist = reps * c->tiles_per_rep <= (long long)c->persist_capacity;
     }
   }

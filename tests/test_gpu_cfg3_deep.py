@@ -6,9 +6,9 @@ that instance is checked against the oracle only to t = 300, while eps reaches e
 and a 10,000-iteration run spends > 96 % of its iterations past it.  Three of cfg3's replicas
 (r = 3.5, kappa = 0 / 0.5 / 1, seed 0: tests/golden/cfg3_deep_digests.json, written by
 tests/golden/make_cfg3_deep_golden.py from the oracle) are stepped here 1,000 iterations on the
-device MT19937 stream with that instance forced (SPGG_APT=max, SPGG_PERSIST=0 -- a 3-replica
-batch would otherwise take two agents per thread in persistent launches, which the second case
-checks): final S, R, Q, the RandomState key after the run and the exact histories bit for bit,
+device MT19937 stream with that instance forced (SPGG_APT=max: a 3-replica batch would otherwise
+take two agents per thread; the second case runs the same replicas in persistent launches,
+SPGG_PERSIST=1): final S, R, Q, the RandomState key after the run and the exact histories bit for bit,
 the float histories within 1e-5 (north_star).  Reference: spgg.py:368-592 (the loop body),
 477-509 (the NI record the kernel recomputes)."""
 import hashlib
@@ -41,7 +41,7 @@ def test_cfg3_replicas_1000_iterations_vs_oracle(mode, monkeypatch):
         monkeypatch.setenv("SPGG_PERSIST", "0")
     else:
         monkeypatch.delenv("SPGG_APT", raising=False)
-        monkeypatch.delenv("SPGG_PERSIST", raising=False)
+        monkeypatch.setenv("SPGG_PERSIST", "1")
     reps = [ReplicaParams(**p) for p in case["replica_params"]]
     eng = BatchEngine(L, T, reps, use_second_order=False, rng="mt19937")
     try:

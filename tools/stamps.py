@@ -1,6 +1,6 @@
 """Phase timeline of one step launch from a -DSPGG_STAMPS=1 build (one stream).
 
-    python tools/stamps.py build_ablate/stamps.so [--config cfg3]
+    python tools/stamps.py build_probe/stamps.so [--config cfg3]
 
 Stamps (s_memrealtime, 10 ns) per workgroup: 0 start, 1 loads staged, 2 phase 1a
 done, 3 phase 1b done, 4 ring barrier passed, 5 phase 2 done, 6 reductions'
@@ -34,13 +34,13 @@ def main():
     eng.step(args.t + 2)
     torch.cuda.synchronize()
     h = ctypes.CDLL(lib)
-    n = 8192 * 10
+    n = 8192 * 12   # (kStampSlots: 0-7 phases, 8 HW_ID, 9 XCC_ID, 10-11 persistent barrier)
     buf = np.zeros(n, dtype=np.uint64)
     rc = h.spgg_stamps_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
     assert rc == 0, rc
     eng.close()
     nwg = len(reps) * eng.tiles_per_rep if hasattr(eng, "tiles_per_rep") else 4200
-    s = buf.reshape(-1, 10)[:nwg].astype(np.int64)
+    s = buf.reshape(-1, 12)[:nwg].astype(np.int64)
     s = s[s[:, 0] > 0]
     t0 = s[:, 0].min()
     st = (s[:, :8] - t0) * 10 / 1000.0  # us
@@ -51,6 +51,14 @@ def main():
     for k, nm in enumerate(names):
         print(f"{nm:15s} {d[:, k].mean():6.2f} {np.percentile(d[:, k], 10):5.2f} {np.percentile(d[:, k], 50):5.2f} "
               f"{np.percentile(d[:, k], 90):5.2f}")
+    if (s[:, 11] > 0).any():   # persistent launch: the replica barrier after iteration t
+        b = (s[:, 10:12] - t0) * 10 / 1000.0
+        drain, wait = b[:, 0] - st[:, 7], b[:, 1] - b[:, 0]
+        for nm, x in (("bar: drain", drain), ("bar: wait", wait)):
+            print(f"{nm:15s} {x.mean():6.2f} {np.percentile(x, 10):5.2f} {np.percentile(x, 50):5.2f} "
+                  f"{np.percentile(x, 90):5.2f}")
+        print(f"barrier passed: first {b[:, 1].min():.2f} last {b[:, 1].max():.2f} us; last arrival "
+              f"{b[:, 0].max():.2f} us")
     life = st[:, 7] - st[:, 0]
     print(f"lifetime        {life.mean():6.2f} {np.percentile(life, 10):5.2f} {np.percentile(life, 50):5.2f} "
           f"{np.percentile(life, 90):5.2f}")

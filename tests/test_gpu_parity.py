@@ -478,12 +478,15 @@ def test_cache_blocked_waves_match_concurrent_groups(rng, monkeypatch):
     L, T = 30, 61
     reps = [_runner_params(r=1.5 + 0.4 * s, influence_factor=0.5 * (s % 3), seed=40 + s) for s in range(10)]
     res = {}
+    per_replica = None
     for mode in ("resident", "waves"):
         if mode == "waves":
-            # 10 x ~36 KB of state (Q-learning recomputes its pending NI record: no md / atd): 3 waves
-            monkeypatch.setenv("SPGG_CACHE_MB", "0.15")
+            # a cache budget of 4 replicas' state (the engine's own per-replica figure, whatever the
+            # kernels keep per agent): ceil(10 / 4) = 3 waves
+            monkeypatch.setenv("SPGG_CACHE_MB", repr(4 * per_replica / 2**20))
             monkeypatch.setenv("SPGG_CHUNK", "7")
         eng = BatchEngine(L, T, reps, use_second_order=True, rng=rng, streams=6)
+        per_replica = eng.state_bytes_per_replica()
         if mode == "waves":
             assert eng.waves == 3 and eng.G == 6 and eng.resident == 2, (eng.waves, eng.G, eng.resident)
         else:

@@ -270,6 +270,9 @@ __device__ __forceinline__ T* at(T* base, uint32_t i) {
 #ifndef SPGG_PERSIST_PLAIN  // timing variant: plain hand-off accesses (results may be stale: WRONG)
 #define SPGG_PERSIST_PLAIN 0
 #endif
+#ifndef SPGG_PERSIST_STAGGER  // timing variant: s_sleep(16) x this per stagger rank after each barrier
+#define SPGG_PERSIST_STAGGER 0
+#endif
 #ifndef SPGG_PERSIST_NORECOMP  // timing variant: see step_impl's CARRY
 #define SPGG_PERSIST_NORECOMP 0
 #endif
@@ -1823,6 +1826,9 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
       break;
     }
     STAMP(11);
+#if SPGG_PERSIST_STAGGER  // timing variant: workgroups start the next iteration staggered by (blockIdx/8)%4
+    for (int z = 0; z < ((blockIdx.x >> 3) & 3) * SPGG_PERSIST_STAGGER; ++z) __builtin_amdgcn_s_sleep(16);
+#endif
   }
   }  // iterations
   if constexpr (PERSIST) {

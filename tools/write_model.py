@@ -1,9 +1,10 @@
 """Model of the step kernel's Q write-back bytes per agent-step under write policies / layouts,
 from the oracle's trajectories of cfg3 replicas (CPU; a measurement aid, not a test).
 
-The L2 writes a 64-B block to the fabric if any byte of it is dirty (tools/traffic_calib.hip,
-profiles/r06/traffic_calibration.txt: 16-B stores into every other 16-B slot cost 2x).  Q is held
-in state planes [s][n][2] (16-B rows), so a block is 4 agents' rows of one state.  A launch at
+The L2 writes a 32-B sector to the fabric if any byte of it is dirty (tools/traffic_calib.hip,
+profiles/r06/traffic_calibration.txt: a 16-B store per 32-B sector costs 2x, at a 64-B stride as
+well).  Q is held in state planes [s][n][2] (16-B rows), so a sector is 2 agents' rows of one state
+(the "sec" columns; they reproduce the measured writes, profiles/r06/traffic/README.txt).  A launch at
 iteration t writes, per agent, its TD row (state s_t) and the row its pending NI term of t-1
 changed (state s_{t-1}); policies:
   kappa   the NI row is written whenever kappa != 0 (the kernel through round 6)
@@ -33,7 +34,7 @@ L = 200
 
 
 def blocks(mask, kind):
-    """Number of 64-B blocks holding at least one marked agent (mask: (L, L) bool)."""
+    """64-B units written: blocks (or half-blocks for "sec") holding at least one marked agent."""
     if kind == "row":
         return int(mask.reshape(L, L // 4, 4).any(axis=2).sum())
     if kind == "sec":   # 32-B sectors: 2 agents' rows
@@ -92,7 +93,7 @@ def main():
     with ProcessPoolExecutor(a.procs) as ex:
         res = list(ex.map(run_one, jobs))
     keys = [(pol, kind) for pol in ("kappa", "nu", "td", "swap") for kind in ("row", "sec", "2x2")]
-    print(f"# Q write-back bytes per agent-step, iterations {a.t0}-{a.t1}, L={L}, seed 0 (64-B blocks)")
+    print(f"# Q write-back bytes per agent-step, iterations {a.t0}-{a.t1}, L={L}, seed 0")
     print("%-12s " % "r, kappa" + " ".join("%11s" % f"{p}/{k}" for p, k in keys) + "  switchers  nu!=0")
     for (rk, v, e) in res:
         print("%-12s " % (f"{rk[0]}, {rk[1]}") + " ".join("%11.2f" % v.get(k, 0.0) for k in keys)

@@ -59,7 +59,7 @@ using namespace spgg;
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
 #endif
-#ifndef SPGG_QSTORE  // A/B probe: 0 changed rows, 1 both rows, 2 rows changed anywhere in the 8-agent line, 3 in the lane pair
+#ifndef SPGG_QSTORE  // A/B probe: 0 changed rows, 1 both rows, 2 rows changed anywhere in the 8-agent line, 3 in the lane pair, 4 in the 8-lane group (DPP)
 #define SPGG_QSTORE 0
 #endif
 // (Rejected A/B knobs -- reward-code pending records, partial Q stores, non-temporal
@@ -1657,6 +1657,12 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
         rows |= (uint32_t)__shfl_xor((int)rows, 4);
 #elif SPGG_QSTORE == 3
         if constexpr (TWC > 0 && TWC % 2 == 0) rows |= partner<1>(rows);
+#elif SPGG_QSTORE == 4
+        if constexpr (TWC > 0 && TWC % 8 == 0) {
+          rows |= partner<1>(rows);
+          rows |= partner<2>(rows);
+          rows |= partner<4>(rows);
+        }
 #endif
         store_q<QB>(Qr, (uint32_t)n, agent_of(rc[u]), q[u], qb[u], rows);
       }

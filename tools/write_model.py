@@ -12,8 +12,9 @@ changed (state s_{t-1}); policies:
   td      TD rows only (an upper bound on what deferring the NI row could give)
   swap    plane 0 holds the row of the agent's current state (a per-agent flag f, swapped -- both
           rows written -- in the launch where s_t != f), plane 1 the other; NI row as "nu"
-blocks: "row" = 4 consecutive agents of a lattice row (the layout), "sec" = the same at 32-B granularity
-(2 agents), "2x2" = a 2x2 agent block.
+units: "sec" = a 32-B sector (2 agents of a lattice row: the hardware's write unit), "row" = a 64-B
+block (4 agents), "line" = a 128-B line (8 agents: what a line-uniform store policy writes), "2x2" =
+a 64-B block of a 2x2 agent block.
 
     python tools/write_model.py [--t0 6 --t1 25] [--replicas 9]
 """
@@ -37,6 +38,8 @@ def blocks(mask, kind):
     """64-B units written: blocks (or half-blocks for "sec") holding at least one marked agent."""
     if kind == "row":
         return int(mask.reshape(L, L // 4, 4).any(axis=2).sum())
+    if kind == "line":  # 128-B lines: 8 agents' rows
+        return 2 * int(mask.reshape(L, L // 8, 8).any(axis=2).sum())
     if kind == "sec":   # 32-B sectors: 2 agents' rows
         return 0.5 * int(mask.reshape(L, L // 2, 2).any(axis=2).sum())
     return int(mask.reshape(L // 2, 2, L // 2, 2).any(axis=(1, 3)).sum())
@@ -59,12 +62,12 @@ def run_one(args):
             f = flag.setdefault("f", ps.copy())
             sw = s != f
             ni_other = (ps != s) & (pnu != 0)
-            for kind in ("row", "sec", "2x2"):
+            for kind in ("sec", "row", "line", "2x2"):
                 n = blocks(np.ones_like(s, dtype=bool), kind) + blocks(sw | ni_other, kind)
                 acc[("swap", kind)] = acc.get(("swap", kind), 0.0) + 64.0 * n / (L * L)
             flag["f"] = s.copy()
             for pol in ("kappa", "nu", "td"):
-                for kind in ("row", "sec", "2x2"):
+                for kind in ("sec", "row", "line", "2x2"):
                     n = 0
                     for plane in (0, 1):
                         m = s == plane
@@ -92,7 +95,7 @@ def main():
     jobs = [(r, k, 0, a.t0, a.t1) for r in (2.0, 3.5, 5.0) for k in (0.0, 0.5, 1.0)]
     with ProcessPoolExecutor(a.procs) as ex:
         res = list(ex.map(run_one, jobs))
-    keys = [(pol, kind) for pol in ("kappa", "nu", "td", "swap") for kind in ("row", "sec", "2x2")]
+    keys = [(pol, kind) for pol in ("kappa", "nu", "td", "swap") for kind in ("sec", "row", "line", "2x2")]
     print(f"# Q write-back bytes per agent-step, iterations {a.t0}-{a.t1}, L={L}, seed 0")
     print("%-12s " % "r, kappa" + " ".join("%11s" % f"{p}/{k}" for p, k in keys) + "  switchers  nu!=0")
     for (rk, v, e) in res:

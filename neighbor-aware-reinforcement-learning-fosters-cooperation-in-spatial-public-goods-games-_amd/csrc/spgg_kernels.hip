@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <type_traits>
 #include <cstdio>
 #include <cstdlib>
@@ -58,6 +59,12 @@ using namespace spgg;
 //   staging and stores, no compute)
 #ifndef SPGG_ABLATE
 #define SPGG_ABLATE 0
+#endif
+#ifndef SPGG_PRIO  // A/B probe: s_setprio of the load phase
+#define SPGG_PRIO 0
+#endif
+#ifndef SPGG_QNT  // A/B probe: bit 0 Q loads, bit 1 Q stores non-temporal (not for Double-Q)
+#define SPGG_QNT 0
 #endif
 #ifndef SPGG_QSTORE  // A/B probe: 0 changed rows, 1 both rows, 2 rows changed anywhere in the 8-agent line, 3 in the lane pair, 4 in the 8-lane group (DPP)
 #define SPGG_QSTORE 0
@@ -101,6 +108,7 @@ struct TileArgs {
   int PB;                 // border-record slots per tile (pub_slots)
   int ring_max;
   int stripes;            // history-record stripes per replica (spgg_stat_stripes)
+  int rep_stride;         // replica of the launch's j-th tile range: (j * rep_stride) % n_rep (rep_stride_for)
 };
 
 // What a step launch needs to pick and size the kernel instance.
@@ -694,7 +702,11 @@ __device__ __forceinline__ void load_q(const double* Qr, uint32_t n, uint32_t ag
                                        double (&qb)[QB ? 4 : 1]) {
   const vd2* q0 = at(reinterpret_cast<const vd2*>(Qr), agent * (QB ? 2 : 1));
   const vd2* q1 = at(reinterpret_cast<const vd2*>(Qr), (n + agent) * (QB ? 2 : 1));
+#if SPGG_QNT & 1  // A/B probe: Q rows loaded non-temporally
+  const vd2 q01 = __builtin_nontemporal_load(q0), q23 = __builtin_nontemporal_load(q1);
+#else
   const vd2 q01 = q0[0], q23 = (SPGG_ABLATE & 4096) ? q01 : q1[0];  // 4096: one plane's reads only
+#endif
   q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
   if constexpr (QB) {
     const vd2 b01 = q0[1], b23 = q1[1];
@@ -708,6 +720,13 @@ __device__ __forceinline__ void store_q(double* Qr, uint32_t n, uint32_t agent, 
                                         const double (&qb)[QB ? 4 : 1], uint32_t rows = 3u) {
   vd2* q0 = at(reinterpret_cast<vd2*>(Qr), agent * (QB ? 2 : 1));
   vd2* q1 = at(reinterpret_cast<vd2*>(Qr), (n + agent) * (QB ? 2 : 1));
+#if SPGG_QNT & 2  // A/B probe: Q rows stored non-temporally
+  if constexpr (!QB) {
+    if (rows & 1u) __builtin_nontemporal_store(vd2{q[0], q[1]}, q0);
+    if (rows & 2u) __builtin_nontemporal_store(vd2{q[2], q[3]}, q1);
+    return;
+  }
+#endif
   if (rows & 1u) {
     q0[0] = vd2{q[0], q[1]};
     if constexpr (QB) q0[1] = vd2{qb[0], qb[1]};
@@ -1053,8 +1072,11 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
   const int logical = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (logical >= total) return;
   if (SPGG_ABLATE & 64) return;
-  const int rep = logical / a0.tiles_per_rep;
-  const int tile = logical - rep * a0.tiles_per_rep;
+  const int lrep = logical / a0.tiles_per_rep;
+  const int tile = logical - lrep * a0.tiles_per_rep;
+  // the XCDs take consecutive tile ranges; a stride over the replicas spreads the cheap ones
+  // (kappa == 0) evenly over them (rep_stride_for)
+  const int rep = a0.rep_stride > 1 ? (int)(((uint32_t)lrep * (uint32_t)a0.rep_stride) % (uint32_t)a0.n_rep) : lrep;
 #if SPGG_STAMPS
   // the workgroup's stamp slot: the batch-wide replica id (stream_id) and tile, so the launches of
   // every replica group (stream) of a batch stamp disjoint slots
@@ -1141,6 +1163,9 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
   RT* Rout = reinterpret_cast<RT*>(a.R_out) + rb;
   const bool pending = t > 1;
   STAMP(0);
+#if SPGG_PRIO  // A/B probe: the load phase at a raised wave priority (back to 0 after staging)
+  if constexpr (!PERSIST) __builtin_amdgcn_s_setprio(SPGG_PRIO);
+#endif
 #if SPGG_STAMPS
   if (t == SPGG_STAMP_T && tid == 0 && stamp_id < kStampWG) {
     unsigned hw, xcc;
@@ -1336,6 +1361,9 @@ __device__ __forceinline__ void step_impl(const TileArgs& a0, const int t0, cons
   }
   __syncthreads();
   STAMP(1);
+#if SPGG_PRIO
+  if constexpr (!PERSIST) __builtin_amdgcn_s_setprio(0);
+#endif
   if (SPGG_ABLATE & 128) {  // memory floor: write back what was read
 #pragma unroll
     for (int u = 0; u < APT; ++u) {
@@ -2606,6 +2634,7 @@ struct spgg_ctx {
   int n = 0;
   int TW = 0, TH = 0, tiles_x = 0, tiles_per_rep = 0, apt = 4, PB = 0;
   int stripes = 1;  // history-record stripes per replica
+  int rep_stride = 1;  // replica order of the step launches over the XCDs (rep_stride_for)
   size_t lds_bytes = 0;
   // persistent launches (spgg_persist_kernel): decided at spgg_create from the whole batch's
   // tiles and the instance's occupancy; arrival counters [n_rep][stripes][kBarWords]
@@ -2858,6 +2887,7 @@ TileArgs make_args(const spgg_ctx* c, int t) {
   a.ring = c->d_ring;
   a.ring_max = c->ring_max;
   a.stripes = c->stripes;
+  a.rep_stride = c->rep_stride;
   return a;
 }
 
@@ -3233,6 +3263,47 @@ int spgg_create(spgg_ctx** out, const spgg_config* cfg) {
   return SPGG_OK;
 }
 
+// The step kernel hands each XCD a consecutive range of logical tiles (blockIdx remap), so the
+// replicas of a launch split over the XCDs in index order.  A replica with kappa == 0 costs ~0.82
+// of another (no NI term: its recomputed record and NI percent are skipped; phase stamps,
+// profiles/r05/phase_stamps_t15_t450.txt), and a batch ordered like the reference's sweeps (kappa in
+// blocks of seeds) gives some XCDs more of them: cfg3's groups 5-7 % above the mean on their
+// busiest XCD.  Logical replica j runs replica (j * stride) % n_rep: the stride (coprime to n_rep)
+// that minimises the busiest XCD's share of that estimate, or 1 when no stride gains >= 1 %.
+// Results do not depend on it (every replica is computed alone).
+static int rep_stride_for(const spgg_ctx* c, const spgg_rep_params* params) {
+  const int R = c->cfg.n_rep, tiles = c->tiles_per_rep;
+  if (R < 3 || tiles < 1) return 1;
+  if (const char* e = tuning_env("SPGG_REP_STRIDE")) {  // tuning knob (a stride not coprime to R: 1)
+    const int st = atoi(e) % R;
+    return st > 1 && std::gcd(st, R) == 1 ? st : 1;
+  }
+  const long long total = (long long)R * tiles, per = (total + 7) / 8;
+  auto busiest = [&](int stride) {
+    double load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < R; ++j) {
+      const int r = (int)(((long long)j * stride) % R);
+      const double w = params[r].kappa == 0.0 ? 0.82 : 1.0;
+      for (long long k = (long long)j * tiles; k < (long long)(j + 1) * tiles;) {  // tiles of j per XCD
+        const int x = (int)(k / per);
+        const long long k1 = std::min((long long)(j + 1) * tiles, (x + 1) * per);
+        load[x] += w * (double)(k1 - k);
+        k = k1;
+      }
+    }
+    return *std::max_element(load, load + 8);
+  };
+  const double base = busiest(1);
+  int best = 1;
+  double best_load = base;
+  for (int st = 2; st < R; ++st) {
+    if (std::gcd(st, R) != 1) continue;
+    const double l = busiest(st);
+    if (l < best_load - 1e-9) { best_load = l; best = st; }
+  }
+  return best_load <= 0.99 * base ? best : 1;
+}
+
 int spgg_set_params(spgg_ctx* c, const spgg_rep_params* params) {
   if (!c || !params) return fail(c, SPGG_E_ARG, "null argument");
   int rc = hip_check(c, hipSetDevice(c->cfg.device), "hipSetDevice");
@@ -3251,6 +3322,7 @@ int spgg_set_params(spgg_ctx* c, const spgg_rep_params* params) {
   if (c->params_host.size() == (size_t)c->cfg.n_rep)
     c->params_moved |= memcmp(c->params_host.data(), params, bytes) != 0;
   c->params_host.assign(params, params + c->cfg.n_rep);
+  c->rep_stride = rep_stride_for(c, params);
   c->params_set = true;
   return SPGG_OK;
 }

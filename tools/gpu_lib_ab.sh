@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of library builds on bench.py's own windows (the driver's 6-25 and the steady 401-600), ONE
 # fresh process per build and round, rounds rotating the order.  Builds: "base" (the in-tree
-# library) or paths of tuning builds (build_ablate/*.so, selected with SPGG_LIB).
+# library), paths of tuning builds (build_probe/*.so, selected with SPGG_LIB), or env:VAR=VALUE (the
+# in-tree library with that tuning knob, under SPGG_TUNING=1).
 # usage: gpu_lib_ab.sh ROUNDS lib... [-- bench args]   -> gpurun_out/lab/lines.txt + a median table
 cd "$GRAFT_REPO_ROOT"; O="$GRAFT_REPO_ROOT/gpurun_out/lab"; mkdir -p "$O"; export TMPDIR=/tmp
 R=$1; shift; LIBS=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do LIBS+=("$1"); shift; done
@@ -10,9 +11,13 @@ for r in $(seq 1 $R); do
   n=${#LIBS[@]}
   for i in $(seq 0 $((n - 1))); do
     L=${LIBS[$(( (i + r) % n ))]}
-    tag=$(basename "$L" .so)
-    if [ "$L" = base ]; then env_lib=""; else env_lib="$GRAFT_REPO_ROOT/$L"; fi
-    SPGG_LIB="$env_lib" timeout -k 10 180 python bench.py --no-cpu-baseline --no-mt --full-run 0 "$@" > "$O/tmp.json" 2> "$O/tmp.err" \
+    tag=$(basename "$L" .so); env_lib=""; env_kv=""
+    case "$L" in
+      base) ;;
+      env:*) env_kv="${L#env:}"; tag="$env_kv" ;;   # the in-tree library with a tuning knob set
+      *) env_lib="$GRAFT_REPO_ROOT/$L" ;;
+    esac
+    env SPGG_LIB="$env_lib" ${env_kv:+SPGG_TUNING=1 "$env_kv"} timeout -k 10 180 python bench.py --no-cpu-baseline --no-mt --full-run 0 "$@" > "$O/tmp.json" 2> "$O/tmp.err" \
       || { echo "$tag failed"; tail -5 "$O/tmp.err"; exit 1; }
     python - "$O/tmp.json" "$tag" "$r" >> "$O/lines.txt" <<'PY'
 import json, sys

@@ -1030,6 +1030,9 @@ constexpr int min_waves(bool m2, int rng, int twc, int alg) {
 #ifdef SPGG_MIN_WAVES
   return SPGG_MIN_WAVES;
 #else
+#ifdef SPGG_MT_MIN_WAVES
+  if (!m2 && rng == SPGG_RNG_MT19937 && twc > 0 && alg != SPGG_ALG_DOUBLE_Q) return SPGG_MT_MIN_WAVES;
+#endif
   return (!m2 && rng == SPGG_RNG_PHILOX && twc > 0 && alg != SPGG_ALG_DOUBLE_Q) ? 4 : 1;
 #endif
 }
@@ -2181,28 +2184,37 @@ __host__ __device__ inline int64_t draw_words_of(int n, int alg) {
 // One recurrence wave and three output waves per chain: the A/B variants of this layout
 // (2 recurrence waves, 1-3 output waves, publication periods, wave priorities, VGPR caps,
 // timing ablations) were measured in round 3 and live in profiles/r03/rejected_gen_knobs.patch.
-constexpr int kGenOut = 3;                       // output waves
+#ifndef SPGG_GEN_OUT
+#define SPGG_GEN_OUT 3
+#endif
+constexpr int kGenOut = SPGG_GEN_OUT;            // output waves
 constexpr int kGenSPW = 4;                       // slots of the lone recurrence wave
 // Blocks between two progress publications of the recurrence wave (each publication waits
 // for the wave's LDS writes: one exposed LDS round trip per period).
 constexpr int kGenPub = 4;
 
-// Chunks between two publications of an output wave's need (the recurrence may run kGenNB - 1 blocks
-// past the smallest need; a wave's need lags its reads by < 2 x 3 x 128 words).
-constexpr int kGenNeedEvery = 2;
+// Chunks an output wave handles per batch (one wait, one need publication, one store of the
+// batch's draw words; the ring coordinates stepped, not divided, from one chunk to the next).
+constexpr int kGenU = 4;
 constexpr int kGenThreads = 64 * (1 + kGenOut);
 constexpr int kMtBlock = 227;                    // 624 - 397: words one dependency step produces
-constexpr int kGenPitch = 256;                   // ring words per block (227 used, 29 of padding)
+// Ring words per block: none of padding, so a chunk's words are contiguous across a block
+// boundary (and into the mirror of block 0 past the last block): one lane address per read.
+constexpr int kGenPitch = kMtBlock;
 // Ring blocks.  Not a lever: 8 or 12 (10 / 14 KB of LDS instead of 18) measured the same whole runs
 // (profiles/r04/generator_groups.txt) -- with the generator resident, the step kernel's occupancy
 // is bound by VGPRs, not LDS.
-constexpr int kGenNB = 16;
-static_assert(kGenNB == 16, "the block loop is unrolled kGenNB times");
+#ifndef SPGG_GEN_NB
+#define SPGG_GEN_NB 16
+#endif
+constexpr int kGenNB = SPGG_GEN_NB;
+static_assert(kGenNB == 16 || kGenNB == 8, "the block loop is unrolled kGenNB times");
 static_assert(kGenNB % kGenPub == 0, "publication period divides the unrolled block loop");
-// an output wave reads at most 2 x 3 x 128 - 1 words past its published need; the frontier it is
-// guaranteed to see lies (kGenNB - kGenPub) x 227 + 1 words past the smallest need
-static_assert(2 * kGenOut * 128 - 1 < (kGenNB - kGenPub) * kMtBlock + 1, "output waves' progress");
-constexpr int kGenRing = kGenPitch * (kGenNB + 1);  // + a mirror of block 0 behind the last one
+// an output wave reads at most kGenU x kGenOut x 128 - 1 words past its published need (a batch);
+// the frontier it is guaranteed to see lies (kGenNB - kGenPub) x 227 + 1 words past the smallest need
+static_assert(kGenU * kGenOut * 128 - 1 < (kGenNB - kGenPub) * kMtBlock + 1, "output waves' progress");
+constexpr int kGenRingWords = kGenPitch * kGenNB;
+constexpr int kGenRing = kGenRingWords + kGenPitch;  // + a mirror of block 0 behind the last one
 // Progress a failed recurrence wave publishes: every output wave's wait then ends at once.
 constexpr uint32_t kGenDoneAbort = (0xffffffffu - 624u) / kMtBlock;
 // Bound of every wait loop between the generator's waves (0.2-0.5 s of s_sleep): a wait that
@@ -2212,22 +2224,26 @@ constexpr uint32_t kGenDoneAbort = (0xffffffffu - 624u) / kMtBlock;
 // stops, so the kernel ends instead of hanging the GPU.  (The recurrence wave stops through its
 // last-block path: an early return there took the kernel from 51 to 74 VGPRs.)
 constexpr uint32_t kGenSpinMax = 1u << 23;
+#ifndef SPGG_GEN_SLEEP_OUT  // s_sleep argument of a polling output wave (x 64 clocks)
+#define SPGG_GEN_SLEEP_OUT 1
+#endif
+#ifndef SPGG_GEN_SLEEP_REC  // s_sleep argument of the recurrence wave waiting for the output waves
+#define SPGG_GEN_SLEEP_REC 2
+#endif
 
 // The 227 positions of a block in 4 slots of 64 lanes: slot s holds positions
 // base(s) + lane for lane < len(s).  Positions 169-226 need positions 0-57 of the block two
 // back (every other position only blocks three back), so slots 0 and 1 -- the same wave --
 // hold both: a wave reads another wave's words only from blocks >= 2 behind, which leaves
-// each wave a block of slack.  The lanes past len(s) (29 = 256 - 227 of them) own the
-// padding positions 227-255, so every LDS write is unconditional.
+// each wave a block of slack.  The lanes past len(s) (29 = 256 - 227 of them) DUPLICATE lane
+// (lane - len(s)) of their slot -- the same position, operands and previous word, so they compute
+// and write the same value to the same address -- so every LDS write is unconditional and the
+// ring has no padding.
 __host__ __device__ constexpr int gen_slot_base(int s) { return s == 0 ? 0 : s == 1 ? 169 : s == 2 ? 58 : 122; }
 __host__ __device__ constexpr int gen_slot_len(int s) { return s == 0 ? 58 : s == 1 ? 58 : s == 2 ? 64 : 47; }
-__host__ __device__ constexpr int gen_slot_pad(int s) { return s == 0 ? 227 : s == 1 ? 233 : 239; }
 __device__ __forceinline__ int gen_position(int s, int lane) {
-  return lane < gen_slot_len(s) ? gen_slot_base(s) + lane : gen_slot_pad(s) + lane - gen_slot_len(s);
+  return gen_slot_base(s) + (lane < gen_slot_len(s) ? lane : lane - gen_slot_len(s));
 }
-// Ring position of block-relative offset o (< 454) of ring block B: a spill past 227 is the
-// next block's start, 29 words further (block kGenNB lands on the mirror of block 0).
-__device__ __forceinline__ uint32_t gen_spill(uint32_t o) { return o + (o >= (uint32_t)kMtBlock ? kGenPitch - kMtBlock : 0u); }
 
 struct GenArgs {
   const uint32_t* key_in;  // [rep][625] chain 0's key + pos: mt_state, or the chunk's key buffer
@@ -2274,9 +2290,10 @@ __device__ __forceinline__ void gen_fail(const GenArgs& g) {
 
 // Word k of a launch (the key block = words 0..623) lives in ring block (k + 57) / 227 - 3
 // (mod kGenNB), at offset (k + 57) % 227: blocks b >= 0 hold words 624 + 227 b ..
+// (blocks are contiguous, so that is ring position (k - 624) mod kGenRingWords)
 __device__ __forceinline__ uint32_t gen_word_pos(uint32_t k) {
-  const uint32_t kk = k + 57, B = kk / kMtBlock;
-  return (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB) + (kk - B * kMtBlock);
+  static_assert(kGenPitch == kMtBlock, "contiguous ring blocks");
+  return (k + (uint32_t)(kGenRingWords - 624)) % (uint32_t)kGenRingWords;
 }
 
 // Iterations t0..t1 of every replica, from its key; writes the draw records, the key
@@ -2348,8 +2365,8 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     for (int i = 0; i < kGenSPW; ++i) {
       const int j = gen_position(i, lane);
       wp[i] = ring + j;
-      pa[i] = ring + gen_spill(j + 57);
-      pb[i] = ring + gen_spill(j + 58);
+      pa[i] = ring + j + 57;  // (a word past 227 is the next block's: contiguous ring)
+      pb[i] = ring + j + 58;
       prev[i] = wp[i][(kGenNB - 1) * kGenPitch];  // x[397 + j]: block -1
       ca[i] = pa[i][(kGenNB - 3) * kGenPitch];    // operands of block 0: block -3
       cb[i] = pb[i][(kGenNB - 3) * kGenPitch];
@@ -2391,7 +2408,7 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       m = __builtin_amdgcn_readfirstlane(m);                                                              \
       /* (saturating: finished output waves publish 0xffffffff) */                                       \
       lim = m > 0xffffffffu - (kGenNB - 1) * kMtBlock ? 0xffffffffu : m + (kGenNB - 1) * kMtBlock;        \
-      if (F > lim) __builtin_amdgcn_s_sleep(2);                                                           \
+      if (F > lim) __builtin_amdgcn_s_sleep(SPGG_GEN_SLEEP_REC);                                          \
     }                                                                                                     \
     if (F > lim) { /* the bound ran out (the condition, not the counter: a last poll that succeeds    \
                       is no failure); this block is the last: rec_done publishes kGenDoneAbort */       \
@@ -2420,8 +2437,10 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     for (;;) {
       SPGG_GEN_BLOCK(0) SPGG_GEN_BLOCK(1) SPGG_GEN_BLOCK(2) SPGG_GEN_BLOCK(3)
       SPGG_GEN_BLOCK(4) SPGG_GEN_BLOCK(5) SPGG_GEN_BLOCK(6) SPGG_GEN_BLOCK(7)
+#if SPGG_GEN_NB == 16
       SPGG_GEN_BLOCK(8) SPGG_GEN_BLOCK(9) SPGG_GEN_BLOCK(10) SPGG_GEN_BLOCK(11)
       SPGG_GEN_BLOCK(12) SPGG_GEN_BLOCK(13) SPGG_GEN_BLOCK(14) SPGG_GEN_BLOCK(15)
+#endif
     }
 #undef SPGG_GEN_BLOCK
   rec_done:
@@ -2436,15 +2455,18 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
     return;
   }
   // ---- output waves: chunks ow, ow + kGenOut, ... of every plane of every iteration --------
-  // (per chunk: one ring read per lane, the temper / parity, one ballot, one two-lane store;
-  // the chunk's first word is published as the wave's need every kGenNeedEvery chunks)
+  // (per chunk: one ring read per lane, the temper / parity, one ballot; per batch of kGenU
+  // chunks: one wait, the batch's first word published as the wave's need, one store)
   const int ow = wave - 1;
   const uint64_t thr_half = u53_threshold(0.5);
   const int nchunk = (g.n + 63) / 64;
   uint32_t kpos = pos0;
   uint32_t seen = 624;  // the frontier as last read
-  uint32_t k = 0;       // chunks this wave has handled
-  const uint32_t lane_planes = (uint32_t)(lane * planes);
+  // lane 2u + h of a batch's store: half h of the draw word of the batch's chunk u
+  // (the record's word of chunk c, plane p, half h: 2 c planes + h planes + p, spgg_abi.h)
+  const uint32_t lane_off = (uint32_t)(((lane >> 1) * kGenOut * 2 + (lane & 1)) * planes);
+  // the draws of the plane's last chunk (n % 64 of them when partial)
+  const uint64_t tail = (g.n & 63) ? (1ull << (g.n & 63)) - 1ull : ~0ull;
   for (int t = t0; t <= t1; ++t) {
     const uint64_t thr = u53_threshold(g.eps[(size_t)rep * g.eps_slots + t]);
     uint32_t* rec_out = g.draws + (size_t)((t - 1) % g.draw_slots) * g.draw_stride + (size_t)rep * g.draw_words;
@@ -2459,18 +2481,24 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
       // (the chunk loop is instantiated per plane kind: the kind's branches leave the loop)
       auto chunks = [&](auto dbl_c) -> bool {
         constexpr bool dbl = decltype(dbl_c)::value;
-        constexpr uint32_t wstep = dbl ? 128u : 64u;
-        const uint32_t wlane = dbl ? 2u * lane : (uint32_t)lane;
-        for (int c = ow; c < nchunk; c += kGenOut, ++k) {
-          const int cnt = min(64, g.n - 64 * c);
-          const uint32_t first = base + wstep * (uint32_t)c;
-          const uint32_t last = first + (dbl ? 2u : 1u) * (uint32_t)cnt - 1u;
-          if (k % kGenNeedEvery == 0) LDS_ST(gen_need[ow][lane], first);
+        constexpr uint32_t wmul = dbl ? 2u : 1u;           // words per draw
+        constexpr uint32_t cstep = 64u * wmul * kGenOut;    // words from one chunk of this wave to its next
+        static_assert(cstep * kGenU < (uint32_t)kGenRingWords, "a batch stays within one turn of the ring");
+        const uint32_t wlane = wmul * (uint32_t)lane;
+        // the current chunk's first word and its ring position, stepped per chunk: word k sits at
+        // (k - 624) mod kGenRingWords (gen_word_pos; the blocks are contiguous)
+        uint32_t first = base + 64u * wmul * (uint32_t)ow;
+        uint32_t rpos = gen_word_pos(first);
+        for (int c = ow; c < nchunk; c += kGenOut * kGenU) {
+          const int nb = min(kGenU, (nchunk - 1 - c) / kGenOut + 1);  // chunks of this batch
+          const int cl = c + (nb - 1) * kGenOut;
+          const uint32_t last = first + cstep * (uint32_t)(nb - 1) + wmul * (uint32_t)min(64, g.n - 64 * cl) - 1u;
+          LDS_ST(gen_need[ow][lane], first);
           if (seen <= last) {  // wait for the recurrence (the check of its bound only on this path)
             uint32_t spin = 0;
             for (; seen <= last && spin < kGenSpinMax; ++spin) {
               seen = 624u + kMtBlock * __builtin_amdgcn_readfirstlane(LDS_LD(gen_done[0]));
-              if (seen <= last) __builtin_amdgcn_s_sleep(1);
+              if (seen <= last) __builtin_amdgcn_s_sleep(SPGG_GEN_SLEEP_OUT);
             }
             if (seen <= last) {  // (the condition itself: a last poll that succeeds is no failure)
               gen_fail(g);
@@ -2479,22 +2507,37 @@ __global__ __launch_bounds__(kGenThreads) void spgg_mt_gen_kernel(GenArgs g, int
             }
           }
           GEN_FENCE();
-          // the chunk's <= 128 words span at most two ring blocks (the mirror covers the last)
-          const uint32_t kk = first + 57, B = kk / kMtBlock, o0 = kk - B * kMtBlock;
-          const uint32_t* rb = ring + (uint32_t)kGenPitch * ((B + kGenNB - 3) % kGenNB);
-          const uint32_t o = o0 + wlane;
-          const uint32_t x = rb[gen_spill(o)];
-          bool flag;
-          if (dbl) {
-            const uint32_t ah = mt_temper(x) >> 5;
-            flag = ah < th_hi;
-            if (ah == th_hi) flag = (mt_temper(rb[gen_spill(o + 1)]) >> 6) < th_lo;
-          } else {  // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
-            flag = (__builtin_popcount(x & kTemperBit0) & 1) != 0;
+          // the batch's words first (one LDS round trip; a chunk past the batch reads a ring word
+          // it drops), then per chunk: the chunk's <= 128 words are contiguous from its ring position
+          // (past the last block: the mirror of block 0)
+          uint32_t rp[kGenU], x[kGenU];
+#pragma unroll
+          for (int u = 0; u < kGenU; ++u) {
+            rp[u] = u == 0 ? rpos : rp[u - 1] + cstep;
+            if (u > 0) rp[u] -= rp[u] >= (uint32_t)kGenRingWords ? (uint32_t)kGenRingWords : 0u;
+            x[u] = ring[rp[u] + wlane];
           }
-          // (lanes past n read stale words: masked)
-          const uint64_t bits = __builtin_amdgcn_ballot_w64(flag) & (cnt == 64 ? ~0ull : (1ull << cnt) - 1ull);
-          if (lane < 2) *at(rec_out, (uint32_t)(2 * c * planes + p) + lane_planes) = (uint32_t)(lane ? bits >> 32 : bits);
+          uint32_t val = 0;
+#pragma unroll
+          for (int u = 0; u < kGenU; ++u) {
+            if (u < nb) {
+              bool flag;
+              if (dbl) {
+                const uint32_t ah = mt_temper(x[u]) >> 5;
+                flag = ah < th_hi;
+                if (ah == th_hi) flag = (mt_temper(ring[rp[u] + wlane + 1]) >> 6) < th_lo;
+              } else {  // randint(0, 2) = the tempered word's low bit = parity of raw bits 0,3,14,18,22,29
+                flag = (__builtin_popcount(x[u] & kTemperBit0) & 1) != 0;
+              }
+              // (lanes past n read stale words: masked)
+              const uint64_t bits = __builtin_amdgcn_ballot_w64(flag) & (c + u * kGenOut == nchunk - 1 ? tail : ~0ull);
+              val = lane == 2 * u ? (uint32_t)bits : lane == 2 * u + 1 ? (uint32_t)(bits >> 32) : val;
+            }
+          }
+          rpos += cstep * (uint32_t)nb;
+          rpos -= rpos >= (uint32_t)kGenRingWords ? (uint32_t)kGenRingWords : 0u;
+          if (lane < 2 * nb) *at(rec_out, (uint32_t)(2 * c * planes + p) + lane_off) = val;
+          first += cstep * (uint32_t)nb;
         }
         return true;
       };

@@ -451,6 +451,17 @@ class BatchEngine:
             C.check(self.lib.spgg_bind(ctx, b), ctx, "spgg_bind")
             self.groups[-1]["bufs"] = b
         self.streams = streams
+        self._draw_stream = None
+        if self.rng == "mt19937" and self.G > 1 and tuning_env("SPGG_SHARED_DRAW_STREAM", "1") == "1":
+            # one generator stream for every group (spgg_set_draw_stream) instead of one per context:
+            # the groups' generator chunks run one after the other instead of side by side, so half
+            # as many generator workgroups share the CUs with the step launches at any time (cfg3
+            # whole run 68.0 -> 65.9 us/iter, profiles/r06/mt_generator/).  A torch pool stream:
+            # non-blocking, and never on the hardware queue of a CU-masked group stream.
+            self._draw_stream = torch.cuda.Stream(self.dev)
+            for gr in self.groups:
+                C.check(self.lib.spgg_set_draw_stream(gr["ctx"], ctypes.c_void_p(self._draw_stream.cuda_stream)),
+                        gr["ctx"], "spgg_set_draw_stream")
         self.ctx = self.groups[0]["ctx"]
         self.tile = self.layout[0]
         self.mt_layout = self.layout[4]

@@ -3,10 +3,11 @@ spgg_mt_gen_kernel) on the CPU: the recurrence and output waves are restated as 
 that yield at every LDS access, run under random interleavings over a sequentially
 consistent LDS, and their outputs are compared with numpy's RandomState stream.
 
-What it checks is the kernel's index arithmetic (the 256-word ring blocks and their mirror,
-the slot/padding positions gen_slot_*, gen_word_pos, gen_spill, the key-block bookkeeping of
-multi-iteration launches) and its synchronisation (gen_done progress, gen_need flow control,
-the recurrence waves' block-of-slack rule), independent of timing.  The hardware ordering the
+What it checks is the kernel's index arithmetic (the contiguous 227-word ring blocks and their
+mirror, the slot positions gen_slot_* with the spare lanes duplicating real ones, gen_word_pos,
+the output waves' stepped ring position per chunk, the key-block bookkeeping of multi-iteration
+launches) and its synchronisation (gen_done progress, gen_need flow control per batch of
+chunks, the recurrence waves' block-of-slack rule), independent of timing.  The hardware ordering the
 kernel relies on beyond sequential consistency (a flag store waits for the wave's earlier LDS
 writes) is exercised by the -m gpu tests.  (A padding-position bug of the first version of
 this kernel -- slot 3's spare lanes overwriting slot 1's words -- is the kind of defect this
@@ -16,25 +17,21 @@ import random
 import numpy as np
 import pytest
 
-NB, P, MB = 16, 256, 227        # kGenNB, kGenPitch, kMtBlock
-RING = P * (NB + 1)
-
-
-def spill(o):                    # gen_spill
-    return o + (P - MB if o >= MB else 0)
+NB, P, MB = 16, 227, 227        # kGenNB, kGenPitch, kMtBlock
+RING_WORDS = P * NB             # kGenRingWords
+RING = RING_WORDS + P           # + the mirror of block 0
+U_BATCH = 4                     # kGenU
 
 
 def word_pos(k):                 # gen_word_pos
-    kk = k + 57
-    B = kk // MB
-    return P * ((B + NB - 3) % NB) + (kk - B * MB)
+    return (k + RING_WORDS - 624) % RING_WORDS
 
 
-SLOT_BASE, SLOT_LEN, SLOT_PAD = (0, 169, 58, 122), (58, 58, 64, 47), (227, 233, 239, 239)   # gen_slot_*
+SLOT_BASE, SLOT_LEN = (0, 169, 58, 122), (58, 58, 64, 47)   # gen_slot_*
 
 
-def position(s, lane):           # gen_position
-    return SLOT_BASE[s] + lane if lane < SLOT_LEN[s] else SLOT_PAD[s] + lane - SLOT_LEN[s]
+def position(s, lane):           # gen_position: spare lanes duplicate lane - len of their slot
+    return SLOT_BASE[s] + (lane if lane < SLOT_LEN[s] else lane - SLOT_LEN[s])
 
 
 def temper(y):
@@ -54,7 +51,7 @@ def plane_word0(n, p):
     return n * (p // 2 * 3 + (p & 1) * 2)
 
 
-def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4, NEED_EVERY=2):
+def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4):
     rnd = random.Random(seed)
     SPW = 4 // NR
     ring = [0] * RING
@@ -71,8 +68,8 @@ def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4, NEED_EVER
     def rec(r):
         lanes = [(i, lane, position(r * SPW + i, lane)) for i in range(SPW) for lane in range(64)]
         prev = {(i, l): ring[j + (NB - 1) * P] for i, l, j in lanes}
-        ca = {(i, l): ring[spill(j + 57) + (NB - 3) * P] for i, l, j in lanes}
-        cb = {(i, l): ring[spill(j + 58) + (NB - 3) * P] for i, l, j in lanes}
+        ca = {(i, l): ring[j + 57 + (NB - 3) * P] for i, l, j in lanes}
+        cb = {(i, l): ring[j + 58 + (NB - 3) * P] for i, l, j in lanes}
         yield
         E = pos0 + W
         mb = ((E - 1) // 624) * 624
@@ -105,8 +102,8 @@ def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4, NEED_EVER
                 yield
             U = b % NB
             rb = ((U + 1 + NB - 3) % NB) * P
-            na = {(i, l): ring[spill(j + 57) + rb] for i, l, j in lanes}
-            nb_ = {(i, l): ring[spill(j + 58) + rb] for i, l, j in lanes}
+            na = {(i, l): ring[j + 57 + rb] for i, l, j in lanes}
+            nb_ = {(i, l): ring[j + 58 + rb] for i, l, j in lanes}
             yield
             for i, l, j in lanes:
                 x = mt_next(prev[i, l], ca[i, l], cb[i, l])
@@ -132,29 +129,39 @@ def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4, NEED_EVER
 
     def outw(ow):
         nchunk = (n + 63) // 64
-        kpos, seen, k = pos0, 624, 0
+        kpos, seen = pos0, 624
         for t in range(t0, t1 + 1):
             for p in range(planes):
-                for c in range(ow, nchunk, NOUT):
-                    cnt, dbl = min(64, n - 64 * c), (p & 1) == 0
-                    first = kpos + plane_word0(n, p) + (128 if dbl else 64) * c
-                    last = first + (2 if dbl else 1) * cnt - 1
-                    if k % NEED_EVERY == 0:       # the need is published every NEED_EVERY chunks
-                        gen_need[ow] = first
-                        yield
-                    k += 1
+                dbl = (p & 1) == 0
+                wmul = 2 if dbl else 1
+                cstep = 64 * wmul * NOUT
+                first = kpos + plane_word0(n, p) + 64 * wmul * ow
+                rpos = word_pos(first)                    # stepped per chunk, never divided
+                for c in range(ow, nchunk, NOUT * U_BATCH):
+                    nb = min(U_BATCH, (nchunk - 1 - c) // NOUT + 1)
+                    cl = c + (nb - 1) * NOUT
+                    last = first + cstep * (nb - 1) + wmul * min(64, n - 64 * cl) - 1
+                    gen_need[ow] = first                  # the batch's first word, once per batch
+                    yield
                     while seen <= last:
                         seen = 624 + MB * min(gen_done)
                         yield
-                    kk = first + 57
-                    B = kk // MB
-                    o0, rbase = kk - B * MB, P * ((B + NB - 3) % NB)
-                    if dbl:
-                        out[t, p, c] = [(temper(ring[rbase + spill(o0 + 2 * l)]),
-                                         temper(ring[rbase + spill(o0 + 2 * l + 1)])) for l in range(cnt)]
-                    else:
-                        out[t, p, c] = [temper(ring[rbase + spill(o0 + l)]) for l in range(cnt)]
-                    yield
+                    rp = rpos
+                    for u in range(nb):
+                        cu = c + u * NOUT
+                        cnt = min(64, n - 64 * cu)
+                        assert rp == word_pos(first + cstep * u)
+                        if dbl:
+                            out[t, p, cu] = [(temper(ring[rp + 2 * l]), temper(ring[rp + 2 * l + 1]))
+                                             for l in range(cnt)]
+                        else:
+                            out[t, p, cu] = [temper(ring[rp + l]) for l in range(cnt)]
+                        rp += cstep
+                        rp -= RING_WORDS if rp >= RING_WORDS else 0
+                        yield
+                    rpos += cstep * nb
+                    rpos -= RING_WORDS if rpos >= RING_WORDS else 0
+                    first += cstep * nb
             kpos += W
         gen_need[ow] = 0xFFFFFFFF
 
@@ -169,16 +176,16 @@ def run_model(n, planes, t0, t1, key, pos0, seed, NR=1, NOUT=7, PUB=4, NEED_EVER
     return out, keys
 
 
-@pytest.mark.parametrize("NOUT,NEED_EVERY", [(3, 2), (7, 2), (3, 1)])
-@pytest.mark.parametrize("n,planes", [(100, 2), (576, 2), (300, 6), (250, 3)])
-def test_generator_protocol_model(NOUT, NEED_EVERY, n, planes):
+@pytest.mark.parametrize("NOUT", [3, 7, 1])
+@pytest.mark.parametrize("n,planes", [(100, 2), (576, 2), (300, 6), (250, 3), (1000, 2)])
+def test_generator_protocol_model(NOUT, n, planes):
     T = 4
     for seed in range(2):
         rs = np.random.RandomState(seed + 11)
         rs.uniform(size=(seed * 37) % 500)          # start mid-block (pos != 624)
         st = rs.get_state()
         key, pos = [int(x) for x in st[1]], int(st[2])
-        out, keys = run_model(n, planes, 1, T, key, pos, seed, NOUT=NOUT, NEED_EVERY=NEED_EVERY)
+        out, keys = run_model(n, planes, 1, T, key, pos, seed, NOUT=NOUT)
         W = n * (planes // 2 * 3 + (planes & 1) * 2)
         nchunk = (n + 63) // 64
         for t in range(1, T + 1):
@@ -198,13 +205,16 @@ def test_generator_protocol_model(NOUT, NEED_EVERY, n, planes):
             assert ps == int(s[2]) and k == [int(x) for x in s[1]], (seed, t)
 
 
-def test_slot_positions_partition_the_block():
-    """Every (slot, lane) owns its own position: the 227 real positions once each, the 29
-    spare lanes the padding 227-255 (a spare lane writing a real position races its owner)."""
-    pos = [position(s, lane) for s in range(4) for lane in range(64)]
-    assert sorted(pos) == list(range(256))
+def test_slot_positions_cover_the_block():
+    """The real lanes own the 227 positions once each; each of the 29 spare lanes duplicates a
+    real lane OF ITS OWN SLOT (the same instruction: same position, operands and previous word,
+    so the same value written to the same address -- a spare lane of another slot or wave
+    writing a real position would race its owner)."""
     real = [position(s, lane) for s in range(4) for lane in range(SLOT_LEN[s])]
     assert sorted(real) == list(range(MB))
+    for s in range(4):
+        own = {position(s, lane) for lane in range(SLOT_LEN[s])}
+        assert {position(s, lane) for lane in range(SLOT_LEN[s], 64)} <= own
     # slots 0 and 1 (one wave) hold positions 0-57 and 169-226: the positions that need the
     # block two back read only that wave's own words
     assert {position(0, l) for l in range(58)} == set(range(58))
